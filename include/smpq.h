@@ -1,0 +1,111 @@
+/*
+ * smpq.h — C-ABI of libsmpq.so, the MI355X-native (gfx950) semilayer mixed-precision
+ * quantized convolution library.
+ *
+ * Plain pointers and sizes only (no torch types). Every device pointer is owned by the
+ * caller (PyTorch's caching allocator on the Python side); the library never allocates
+ * device memory and keeps no pointer past a call. Every kernel is enqueued on the HIP
+ * stream passed in (Python passes torch.cuda.current_stream().cuda_stream), nothing blocks
+ * the host except the *_host entry points. Return value: 0 on success, a negative SMPQ_E_*
+ * code otherwise; smpq_last_error() holds a thread-local message.
+ *
+ * Reference interfaces replaced (kenm-28/Semilayer-Wise-Mixed-Precision-Quantization):
+ *   smpq_quantize_channels[_host]  functions.py:25-43 quantize_wgt, applied per output channel
+ *                                  as functions.py:9-23 channel_wise_quantizationperchan does
+ *                                  (called from resnet50_main.py:189-197, functions.py:504-512)
+ *   smpq_pack_weights              (new) fake-quantized fp32 weight -> int8 codes + per-channel
+ *                                  step/offset; feeds the conv below (the reference keeps the
+ *                                  fake-quantized fp32 weight in nn.Conv2d, resnet.py:22-30)
+ *   smpq_conv2d_fwd                nn.Conv2d forward on the fake-quantized weight
+ *                                  (resnet.py:22-30 via resnet.py:57,60,99,103,107) fused with
+ *                                  the eval BatchNorm / ReLU / residual add that follow it in
+ *                                  BasicBlock.forward (resnet.py:55-68) / Bottleneck.forward
+ *                                  (resnet.py:97-116)
+ *   smpq_act_absmax                (new) per-image activation range for the activation quantizer
+ */
+#ifndef SMPQ_H_
+#define SMPQ_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SMPQ_ABI_VERSION 1
+
+/* status codes */
+#define SMPQ_OK 0
+#define SMPQ_E_INVALID (-1)  /* bad argument / unsupported configuration */
+#define SMPQ_E_SHAPE (-2)    /* shape the kernels do not support */
+#define SMPQ_E_BITS (-3)     /* bit-width outside {1..8} */
+#define SMPQ_E_RANGE (-4)    /* a channel's codes span more than 256 levels */
+#define SMPQ_E_CONSTANT (-5) /* constant channel: the reference raises ZeroDivisionError */
+#define SMPQ_E_HIP (-6)      /* a HIP runtime call failed */
+#define SMPQ_E_INEXACT (-7)  /* weights are not on the recorded quantization grid */
+
+typedef void* smpq_stream_t; /* hipStream_t */
+
+int smpq_abi_version(void);
+const char* smpq_last_error(void);
+
+/* Fake-quantize channels of w in place, bit-exactly as functions.py:25-43.
+ *   w          device fp32 [cout][k_elems] (one output channel per row)
+ *   bits       device int8 [cout]; 0 leaves the channel untouched
+ *   scale_out  device fp32 [cout]; receives fp32(scale) of the quantization applied
+ *   status     device int32 [1], caller-zeroed; set to (first constant channel)+1 */
+int smpq_quantize_channels(float* w, int cout, int k_elems, const int8_t* bits,
+                           float* scale_out, int32_t* status, smpq_stream_t stream);
+
+/* Host-memory twin of smpq_quantize_channels (same arithmetic, native C++), used when the
+ * weight lives in host memory (the reference quantizes CPU tensors of fresh models, e.g.
+ * functions.py:504-512 right after resnet.resnet50(...) at :528). Returns SMPQ_E_CONSTANT on
+ * a constant channel (channels before it are already quantized, as in the reference loop). */
+int smpq_quantize_channels_host(float* w, int cout, int k_elems, const int8_t* bits,
+                                float* scale_out);
+
+/* Pack fake-quantized weights into the conv kernel's layout.
+ *   w       device fp32 [cout][cin][kh][kw] (fake-quantized, values fl32(m * step))
+ *   step    device fp32 [cout] quantization step (scale_out of the quantizer)
+ *   codes   device int8 [cout][kh][kw][cin]   m - offset, in [-128, 127]
+ *   offset  device int32 [cout]
+ *   status  device int32 [2], caller-zeroed: [0] += channels not on the grid,
+ *           [1] += channels whose codes span > 256 levels */
+int smpq_pack_weights(const float* w, int cout, int cin, int kh, int kw, const float* step,
+                      int8_t* codes, int32_t* offset, int32_t* status, smpq_stream_t stream);
+
+/* Per-image absolute maximum, accumulated with atomicMax into absmax[n] (caller zeroes). */
+int smpq_act_absmax(const float* x, int n, int64_t per_image, float* absmax,
+                    smpq_stream_t stream);
+
+/* Quantized conv forward (implicit GEMM on int8 MFMA), NHWC fp32 in/out.
+ *   x          device fp32 NHWC [n][h][w][cin]; cin % 64 == 0
+ *   x_absmax   device fp32 [n] per-image max|x| (activation quantizer range)
+ *   codes/offset/cout/kh/kw: from smpq_pack_weights
+ *   col_scale  device fp32 [cout]: y = conv_real * col_scale[c] + col_shift[c]
+ *              (col_scale = step * bn_gamma / sqrt(var+eps), col_shift = bn_beta - mean * ...)
+ *   residual   device fp32 NHWC [n][ho][wo][cout] added after the affine, or NULL
+ *   relu       0/1, applied last
+ *   limbs      activation code width in int8 limbs: 1 (int8), 2 (int16), 3 (int24)
+ *   y          device fp32 NHWC [n][ho][wo][cout]
+ *   y_absmax   device fp32 [n] (caller-zeroed), receives max|y| per image, or NULL */
+int smpq_conv2d_fwd(const float* x, const float* x_absmax, int n, int h, int w, int cin,
+                    const int8_t* codes, const int32_t* offset, int cout, int kh, int kw,
+                    int stride, int pad, const float* col_scale, const float* col_shift,
+                    const float* residual, int relu, int limbs, float* y, float* y_absmax,
+                    smpq_stream_t stream);
+
+/* Workspace the conv needs (none today; kept for ABI stability). */
+size_t smpq_conv2d_workspace_bytes(int n, int h, int w, int cin, int cout, int kh, int kw,
+                                   int stride, int pad, int limbs);
+
+/* Diagnostics: one v_mfma_i32_16x16x64_i8 with the kernel's fragment mapping.
+ *   a [16][64] int8 row-major, b [16][64] int8 (b[col][k]), c [16][16] int32 row-major */
+int smpq_debug_mfma_i8(const int8_t* a, const int8_t* b, int32_t* c, smpq_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SMPQ_H_ */

@@ -1,0 +1,449 @@
+// Quantized convolution forward for gfx950 (CDNA4): implicit GEMM on int8 MFMA.
+//
+// Replaces nn.Conv2d on the fake-quantized weight (resnet.py:22-30) together with the eval
+// BatchNorm, ReLU and residual add that follow it (resnet.py:55-68 / 97-116).
+//
+// GEMM view (NHWC activations, K ordered [kh][kw][cin]):
+//   M = n*ho*wo output pixels, N = cout, K = kh*kw*cin (cin % 64 == 0: one 64-wide K step is
+//   64 contiguous input channels of a single tap, i.e. one 256-B fp32 run of one NHWC pixel).
+//   A[m][k] = activation code of x at the tap's input pixel (0 outside the image: zero pad)
+//   B[k][n] = weight code m_n,k - offset_n (int8, from smpq_pack_weights)
+//
+// Exactness of the weight side: the reference weight is w = fl32(m * step) (functions.py:41);
+// the kernel multiplies the integer code m (exact) and applies `step` once per output, so the
+// only weight-side difference is the <= 2^-24 relative rounding inside fl32(m * step).
+//
+// Activation side: x is quantized ON LOAD with a per-image step s_x = max|x_img| / QMAX into
+// an integer q with `L` balanced base-256 int8 digits (limbs): q = sum_l 256^l d_l.
+// L = 1 gives int8, L = 2 int16, L = 3 int24 fixed point; each limb is one MFMA pass over the
+// same B fragment, accumulated in its own int32 accumulator, recombined in fp32 in the epilogue.
+//
+// Tile: 256 threads = 4 waves as 2 (M) x 2 (N); each wave owns WM x WN subtiles of 16 x 16
+// computed with v_mfma_i32_16x16x64_i8 (one K step of 64 per MFMA). Block tile
+// BM = 32*WM rows x BN = 32*WN columns. Global -> register prefetch of step k+1 overlaps the
+// MFMAs of step k; one LDS double buffer, one barrier per K step.
+#include <string>
+
+#include "common.h"
+
+namespace smpq {
+
+constexpr int kThreads = 256;
+constexpr int kKStep = 64;      // K per MFMA (i8 16x16x64)
+constexpr int kRowBytes = 80;   // LDS row stride for a 64-byte K slice (+16 B pad vs conflicts)
+
+struct ConvArgs {
+  const float* x;
+  const float* x_absmax;
+  const int8_t* codes;
+  const int32_t* w_off;
+  const float* col_scale;
+  const float* col_shift;
+  const float* residual;
+  float* y;
+  float* y_absmax;
+  int n, h, w, cin, cout, kh, kw, stride, pad, ho, wo;
+  int M, K, ksteps, cchunks;
+  int relu, has_offset;
+  float qmax, inv_qmax;
+};
+
+template <int L>
+__device__ __forceinline__ void split_limbs(int q, int* d) {
+  // balanced base-256 digits, each in [-128, 127]
+#pragma unroll
+  for (int l = 0; l < L - 1; ++l) {
+    const int lo = ((q + 128) & 255) - 128;
+    d[l] = lo;
+    q = (q - lo) >> 8;
+  }
+  d[L - 1] = q;
+}
+
+template <int L, int WM, int WN>
+__global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
+  constexpr int BM = 32 * WM;
+  constexpr int BN = 32 * WN;
+  constexpr int AROWS = BM / 16;  // A rows loaded per thread per K step (16 threads per row)
+  constexpr int BROWS = BN / 64;  // B rows loaded per thread per K step (4 threads per row)
+
+  __shared__ __attribute__((aligned(16))) int8_t As[2][L][BM][kRowBytes];
+  __shared__ __attribute__((aligned(16))) int8_t Bs[2][BN][kRowBytes];
+  __shared__ float s_rowscale[BM];
+  __shared__ int s_rowimg[BM];
+  __shared__ unsigned int s_rowmax[BM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int ntiles = (a.cout + BN - 1) / BN;
+  const int m0 = (blockIdx.x / ntiles) * BM;
+  const int n0 = (blockIdx.x % ntiles) * BN;
+  const int hw_out = a.ho * a.wo;
+
+  // ---- per-block row table: image index and activation step of each output row ----------
+  for (int r = tid; r < BM; r += kThreads) {
+    const int m = m0 + r;
+    int img = -1;
+    float sc = 0.f;
+    if (m < a.M) {
+      img = m / hw_out;
+      sc = a.x_absmax[img] * a.inv_qmax;
+    }
+    s_rowimg[r] = img;
+    s_rowscale[r] = sc;
+    s_rowmax[r] = 0u;
+  }
+
+  // ---- per-thread A load rows: input pixel base, top-left tap coordinate, 1/step ---------
+  const int apiece = tid & 15;  // 16-B piece of the 256-B fp32 K slice (4 channels)
+  const int arow0 = tid >> 4;   // rows arow0 + 16*i
+  int a_pix[AROWS];             // n*h*w pixel base, or -1 when the row is past M
+  int a_ih[AROWS], a_iw[AROWS];
+  float a_inv[AROWS];
+#pragma unroll
+  for (int i = 0; i < AROWS; ++i) {
+    const int m = m0 + arow0 + 16 * i;
+    if (m < a.M) {
+      const int img = m / hw_out;
+      const int rem = m - img * hw_out;
+      const int oh = rem / a.wo;
+      const int ow = rem - oh * a.wo;
+      a_pix[i] = img * a.h * a.w;
+      a_ih[i] = oh * a.stride - a.pad;
+      a_iw[i] = ow * a.stride - a.pad;
+      const float am = a.x_absmax[img];
+      a_inv[i] = am > 0.f ? a.qmax / am : 0.f;
+    } else {
+      a_pix[i] = -1;
+      a_ih[i] = a_iw[i] = 0;
+      a_inv[i] = 0.f;
+    }
+  }
+  const int bpiece = tid & 3;  // 16-B piece of the 64-B int8 K slice
+  const int brow0 = tid >> 2;  // rows brow0 + 64*j
+
+  float4 ra[AROWS];
+  v4i rb[BROWS];
+
+  auto load_global = [&](int ks) {
+    const int tap = ks / a.cchunks;
+    const int c0 = (ks - tap * a.cchunks) * kKStep;
+    const int kr = tap / a.kw;
+    const int kc = tap - kr * a.kw;
+#pragma unroll
+    for (int i = 0; i < AROWS; ++i) {
+      const int ih = a_ih[i] + kr;
+      const int iw = a_iw[i] + kc;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (a_pix[i] >= 0 && (unsigned)ih < (unsigned)a.h && (unsigned)iw < (unsigned)a.w) {
+        const float* p = a.x + ((size_t)(a_pix[i] + ih * a.w + iw) * a.cin + c0 + 4 * apiece);
+        v = *reinterpret_cast<const float4*>(p);
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < BROWS; ++j) {
+      const int col = n0 + brow0 + 64 * j;
+      v4i v = {0, 0, 0, 0};
+      if (col < a.cout) {
+        v = *reinterpret_cast<const v4i*>(a.codes + (size_t)col * a.K + ks * kKStep + 16 * bpiece);
+      }
+      rb[j] = v;
+    }
+  };
+
+  auto store_lds = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AROWS; ++i) {
+      const float vals[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+      int packed[L];
+#pragma unroll
+      for (int l = 0; l < L; ++l) packed[l] = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float qf = rintf(vals[e] * a_inv[i]);
+        qf = fminf(fmaxf(qf, -a.qmax), a.qmax);
+        int d[L];
+        split_limbs<L>((int)qf, d);
+#pragma unroll
+        for (int l = 0; l < L; ++l) packed[l] |= (d[l] & 255) << (8 * e);
+      }
+      const int r = arow0 + 16 * i;
+#pragma unroll
+      for (int l = 0; l < L; ++l)
+        *reinterpret_cast<int*>(&As[buf][l][r][4 * apiece]) = packed[l];
+    }
+#pragma unroll
+    for (int j = 0; j < BROWS; ++j)
+      *reinterpret_cast<v4i*>(&Bs[buf][brow0 + 64 * j][16 * bpiece]) = rb[j];
+  };
+
+  v4i acc[L][WM][WN];
+  int rs[L][WM];  // per-lane partial row sums of A codes (only for offset correction)
+#pragma unroll
+  for (int l = 0; l < L; ++l)
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      rs[l][i] = 0;
+#pragma unroll
+      for (int j = 0; j < WN; ++j) acc[l][i][j] = v4i{0, 0, 0, 0};
+    }
+
+  load_global(0);
+  store_lds(0);
+  __syncthreads();
+
+  const int frow = lane & 15;         // fragment row/col owned by this lane
+  const int fk = 16 * (lane >> 4);    // fragment K byte offset owned by this lane
+  const int arow_base = wm * 16 * WM;
+  const int bcol_base = wn * 16 * WN;
+
+  for (int ks = 0; ks < a.ksteps; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < a.ksteps) load_global(ks + 1);
+
+    v4i bf[WN];
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+      bf[j] = *reinterpret_cast<const v4i*>(&Bs[buf][bcol_base + 16 * j + frow][fk]);
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        const v4i af = *reinterpret_cast<const v4i*>(&As[buf][l][arow_base + 16 * i + frow][fk]);
+        if (a.has_offset) {
+          int s = rs[l][i];
+          s = __builtin_amdgcn_sdot4(af.x, 0x01010101, s, false);
+          s = __builtin_amdgcn_sdot4(af.y, 0x01010101, s, false);
+          s = __builtin_amdgcn_sdot4(af.z, 0x01010101, s, false);
+          s = __builtin_amdgcn_sdot4(af.w, 0x01010101, s, false);
+          rs[l][i] = s;
+        }
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          acc[l][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[j], acc[l][i][j], 0, 0, 0);
+      }
+    }
+
+    if (ks + 1 < a.ksteps) store_lds(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: recombine limbs, affine (dequant * BN), residual, ReLU, store, absmax ----
+  // row sums: lanes {l, l^16, l^32, l^48} hold the four K quarters of row (l & 15)
+  if (a.has_offset) {
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        int s = rs[l][i];
+        s += __shfl_xor(s, 16, kWave);
+        s += __shfl_xor(s, 32, kWave);
+        rs[l][i] = s;
+      }
+  }
+
+  float colscale[WN], colshift[WN];
+  int coloff[WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int col = n0 + bcol_base + 16 * j + frow;
+    const bool ok = col < a.cout;
+    colscale[j] = ok ? a.col_scale[col] : 0.f;
+    colshift[j] = ok ? a.col_shift[col] : 0.f;
+    coloff[j] = (ok && a.has_offset) ? a.w_off[col] : 0;
+  }
+
+#pragma unroll
+  for (int i = 0; i < WM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rloc = arow_base + 16 * i + 4 * (lane >> 4) + r;  // C layout: row = 4*(lane>>4)+reg
+      const int m = m0 + rloc;
+      const float rscale = s_rowscale[rloc];
+      int rsum[L];
+#pragma unroll
+      for (int l = 0; l < L; ++l)
+        rsum[l] = a.has_offset ? __shfl(rs[l][i], 4 * (lane >> 4) + r, kWave) : 0;
+      float rmax = 0.f;
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        const int col = n0 + bcol_base + 16 * j + frow;
+        float v = 0.f;
+        float limbw = 1.f;
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+          const int t = acc[l][i][j][r] + coloff[j] * rsum[l];
+          v += (float)t * limbw;
+          limbw *= 256.f;
+        }
+        float out = v * (rscale * colscale[j]) + colshift[j];
+        if (m < a.M && col < a.cout) {
+          const size_t idx = (size_t)m * a.cout + col;
+          if (a.residual) out += a.residual[idx];
+          if (a.relu) out = fmaxf(out, 0.f);
+          a.y[idx] = out;
+          rmax = fmaxf(rmax, fabsf(out));
+        }
+      }
+      if (a.y_absmax) {
+        // reduce over the 16 lanes (columns) that share this row
+        rmax = fmaxf(rmax, __shfl_xor(rmax, 1, kWave));
+        rmax = fmaxf(rmax, __shfl_xor(rmax, 2, kWave));
+        rmax = fmaxf(rmax, __shfl_xor(rmax, 4, kWave));
+        rmax = fmaxf(rmax, __shfl_xor(rmax, 8, kWave));
+        if (frow == 0 && m < a.M) atomicMax(&s_rowmax[rloc], __float_as_uint(rmax));
+      }
+    }
+  }
+
+  if (a.y_absmax) {
+    __syncthreads();
+    if (wave == 0) {
+      const int img_lo = s_rowimg[0];
+      int last = min(BM, a.M - m0) - 1;
+      const int img_hi = s_rowimg[last];
+      for (int img = img_lo; img <= img_hi; ++img) {
+        float v = 0.f;
+        for (int r = lane; r < BM; r += kWave)
+          if (s_rowimg[r] == img) v = fmaxf(v, __uint_as_float(s_rowmax[r]));
+        v = wave_max(v);
+        if (lane == 0 && v > 0.f) atomic_max_nonneg(&a.y_absmax[img], v);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, int64_t per_image,
+                                                     float* __restrict__ out) {
+  const int img = blockIdx.y;
+  const float* p = x + (size_t)img * per_image;
+  float m = 0.f;
+  const int64_t start = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  if ((per_image & 3) == 0) {
+    for (int64_t i = start; i < per_image; i += stride) {
+      const float4 v = *reinterpret_cast<const float4*>(p + i);
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+  } else {
+    for (int64_t i = start / 4 + 0; i < per_image; i += stride / 4) m = fmaxf(m, fabsf(p[i]));
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0 && m > 0.f) atomic_max_nonneg(&out[img], m);
+}
+
+__global__ void debug_mfma_kernel(const int8_t* a, const int8_t* b, int32_t* c) {
+  const int lane = threadIdx.x;
+  const int frow = lane & 15, fk = 16 * (lane >> 4);
+  const v4i af = *reinterpret_cast<const v4i*>(a + frow * 64 + fk);
+  const v4i bf = *reinterpret_cast<const v4i*>(b + frow * 64 + fk);
+  v4i acc = {0, 0, 0, 0};
+  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf, acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) c[(4 * (lane >> 4) + r) * 16 + frow] = acc[r];
+}
+
+template <int L, int WM, int WN>
+static int launch(const ConvArgs& a, hipStream_t stream) {
+  constexpr int BM = 32 * WM, BN = 32 * WN;
+  const long mt = (a.M + BM - 1) / BM;
+  const long nt = (a.cout + BN - 1) / BN;
+  const long blocks = mt * nt;
+  if (blocks > 0x7fffffffL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
+  hipLaunchKernelGGL((qconv_kernel<L, WM, WN>), dim3((unsigned)blocks), dim3(kThreads), 0, stream, a);
+  return check_hip(hipGetLastError(), "qconv_kernel launch");
+}
+
+}  // namespace smpq
+
+using namespace smpq;
+
+extern "C" int smpq_conv2d_fwd(const float* x, const float* x_absmax, int n, int h, int w, int cin,
+                               const int8_t* codes, const int32_t* offset, int cout, int kh, int kw,
+                               int stride, int pad, const float* col_scale, const float* col_shift,
+                               const float* residual, int relu, int limbs, float* y, float* y_absmax,
+                               smpq_stream_t stream) {
+  if (!x || !x_absmax || !codes || !col_scale || !col_shift || !y)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: null pointer");
+  if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || stride <= 0 ||
+      pad < 0)
+    return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: bad shape");
+  if (cin % kKStep != 0)
+    return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: cin must be a multiple of 64 (got " +
+                                  std::to_string(cin) + ")");
+  ConvArgs a;
+  a.x = x;
+  a.x_absmax = x_absmax;
+  a.codes = codes;
+  a.w_off = offset;
+  a.col_scale = col_scale;
+  a.col_shift = col_shift;
+  a.residual = residual;
+  a.y = y;
+  a.y_absmax = y_absmax;
+  a.n = n;
+  a.h = h;
+  a.w = w;
+  a.cin = cin;
+  a.cout = cout;
+  a.kh = kh;
+  a.kw = kw;
+  a.stride = stride;
+  a.pad = pad;
+  a.ho = (h + 2 * pad - kh) / stride + 1;
+  a.wo = (w + 2 * pad - kw) / stride + 1;
+  if (a.ho <= 0 || a.wo <= 0) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: empty output");
+  const long M = (long)n * a.ho * a.wo;
+  if (M > 0x7fffffffL || (long)n * h * w * (long)cin > 0x7fffffffL * 4L)
+    return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: tensor too large");
+  a.M = (int)M;
+  a.K = kh * kw * cin;
+  a.cchunks = cin / kKStep;
+  a.ksteps = kh * kw * a.cchunks;
+  a.relu = relu ? 1 : 0;
+  a.has_offset = offset ? 1 : 0;
+  hipStream_t s = (hipStream_t)stream;
+  switch (limbs) {
+    case 1:
+      a.qmax = 127.f;
+      a.inv_qmax = 1.f / 127.f;
+      return cout <= 64 ? launch<1, 4, 2>(a, s) : launch<1, 4, 4>(a, s);
+    case 2:
+      a.qmax = 32512.f;
+      a.inv_qmax = 1.f / 32512.f;
+      return launch<2, 4, 2>(a, s);
+    case 3:
+      a.qmax = 8323072.f;
+      a.inv_qmax = 1.f / 8323072.f;
+      return launch<3, 4, 2>(a, s);
+    default:
+      return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: limbs must be 1, 2 or 3");
+  }
+}
+
+extern "C" size_t smpq_conv2d_workspace_bytes(int, int, int, int, int, int, int, int, int, int) {
+  return 0;
+}
+
+extern "C" int smpq_act_absmax(const float* x, int n, int64_t per_image, float* absmax,
+                               smpq_stream_t stream) {
+  if (!x || !absmax || n <= 0 || per_image <= 0)
+    return fail(SMPQ_E_INVALID, "smpq_act_absmax: bad arguments");
+  int chunks = (int)((per_image / 4 + 255) / 256);
+  if (chunks > 64) chunks = 64;
+  if (chunks < 1) chunks = 1;
+  hipLaunchKernelGGL(absmax_kernel, dim3(chunks, n), dim3(256), 0, (hipStream_t)stream, x, per_image,
+                     absmax);
+  return check_hip(hipGetLastError(), "absmax_kernel launch");
+}
+
+extern "C" int smpq_debug_mfma_i8(const int8_t* a, const int8_t* b, int32_t* c, smpq_stream_t stream) {
+  if (!a || !b || !c) return fail(SMPQ_E_INVALID, "smpq_debug_mfma_i8: null pointer");
+  hipLaunchKernelGGL(debug_mfma_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, c);
+  return check_hip(hipGetLastError(), "debug_mfma_kernel launch");
+}

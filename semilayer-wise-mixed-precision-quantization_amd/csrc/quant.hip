@@ -1,0 +1,197 @@
+// Weight fake-quantizer (bit-exact with the reference) and the int8 code packer.
+//
+// Reference arithmetic (functions.py:25-43, quantize_wgt), per output channel t:
+//   mn, mx  = exact fp32 min / max of t                      (functions.py:35-36, .item())
+//   scale   = (mx - mn) / (2^bit - 1)           IEEE double   (functions.py:39)
+//   z       = round(mn / scale)                 half-even      (functions.py:40)
+//   q       = (rne(t / f32(scale) + f32(z)) - f32(z)) * f32(scale)   fp32 ops (functions.py:41)
+// `t / f32(scale)` is a correctly rounded fp32 division (torch CPU divides; it does not
+// multiply by a reciprocal), so the device code uses __fdiv_rn and FP contraction is off.
+//
+// One workgroup per output channel: channels are at most 4608 elements (R50 layer4 conv2),
+// so a 256-thread block covers a channel in <= 18 iterations and the launch is a single
+// wave of blocks over all channels of a layer (22,656 channels for all of ResNet-50).
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace smpq {
+
+constexpr int kQThreads = 256;
+
+__device__ __forceinline__ void block_minmax(float& mn, float& mx, float* smem) {
+  // smem: 2 * (kQThreads / 64) floats
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  if (lane == 0) {
+    smem[wid] = mn;
+    smem[kQThreads / kWave + wid] = mx;
+  }
+  __syncthreads();
+  mn = smem[0];
+  mx = smem[kQThreads / kWave];
+#pragma unroll
+  for (int i = 1; i < kQThreads / kWave; ++i) {
+    mn = fminf(mn, smem[i]);
+    mx = fmaxf(mx, smem[kQThreads / kWave + i]);
+  }
+}
+
+__global__ __launch_bounds__(kQThreads) void quantize_channels_kernel(
+    float* __restrict__ w, int k, const int8_t* __restrict__ bits, float* __restrict__ scale_out,
+    int32_t* __restrict__ status) {
+  __shared__ float smem[2 * kQThreads / kWave];
+  const int c = blockIdx.x;
+  const int b = bits[c];
+  if (b <= 0) return;
+  float* row = w + (size_t)c * k;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int i = threadIdx.x; i < k; i += kQThreads) {
+    const float v = row[i];
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+  }
+  block_minmax(mn, mx, smem);
+  if (mx == mn) {  // reference: ZeroDivisionError at functions.py:40
+    if (threadIdx.x == 0) atomicCAS(reinterpret_cast<int*>(status), 0, c + 1);
+    return;
+  }
+  const double scale = ((double)mx - (double)mn) / (double)((1 << b) - 1);
+  const double zd = rint((double)mn / scale) + 0.0;  // Python round(): half-to-even; no -0
+  const float s32 = (float)scale;
+  const float z32 = (float)zd;
+  for (int i = threadIdx.x; i < k; i += kQThreads) {
+    const float t = row[i];
+    const float q = rintf(__fdiv_rn(t, s32) + z32) - z32;
+    row[i] = __fmul_rn(q, s32);
+  }
+  if (threadIdx.x == 0) scale_out[c] = s32;
+}
+
+// Codes m = rne(w / step) (exact: w = fl32(m * step) with |m| <= 2^9 so |w/step - m| < 2^-14),
+// verified bitwise against fl32(m * step); stored as m - offset in the conv's K order
+// [kh][kw][cin] so one 64-wide K step is 64 contiguous input channels of one tap (NHWC).
+__global__ __launch_bounds__(kQThreads) void pack_weights_kernel(
+    const float* __restrict__ w, int cin, int kh, int kw, const float* __restrict__ step,
+    int8_t* __restrict__ codes, int32_t* __restrict__ offset, int32_t* __restrict__ status) {
+  __shared__ int smem[3 * kQThreads / kWave];
+  const int c = blockIdx.x;
+  const int taps = kh * kw;
+  const int k = cin * taps;
+  const float* row = w + (size_t)c * k;
+  const float s = step[c];
+  int mmin = INT32_MAX, mmax = INT32_MIN, bad = 0;
+  for (int i = threadIdx.x; i < k; i += kQThreads) {
+    const float v = row[i];
+    const float mf = rintf(__fdiv_rn(v, s));
+    if (!(s > 0.f) || __fmul_rn(mf, s) != v || fabsf(mf) > 65536.f) {
+      bad = 1;
+      continue;
+    }
+    const int m = (int)mf;
+    mmin = min(mmin, m);
+    mmax = max(mmax, m);
+  }
+  mmin = wave_min_i(mmin);
+  mmax = wave_max_i(mmax);
+  bad = wave_max_i(bad);
+  const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  if (lane == 0) {
+    smem[wid] = mmin;
+    smem[4 + wid] = mmax;
+    smem[8 + wid] = bad;
+  }
+  __syncthreads();
+  mmin = min(min(smem[0], smem[1]), min(smem[2], smem[3]));
+  mmax = max(max(smem[4], smem[5]), max(smem[6], smem[7]));
+  bad = smem[8] | smem[9] | smem[10] | smem[11];
+  int o = 0;
+  bool range_bad = false;
+  if (!bad) {
+    if (mmax - mmin > 255) range_bad = true;
+    else if (mmin < -128 || mmax > 127) o = mmin + 128;
+  }
+  if (threadIdx.x == 0) {
+    if (bad) atomicAdd(&status[0], 1);
+    if (range_bad) atomicAdd(&status[1], 1);
+    offset[c] = o;
+  }
+  int8_t* out = codes + (size_t)c * k;
+  for (int i = threadIdx.x; i < k; i += kQThreads) {
+    // reference order i = (ci*kh + r)*kw + q ; kernel order j = (r*kw + q)*cin + ci
+    const int ci = i / taps;
+    const int t = i - ci * taps;
+    int m = 0;
+    if (!bad && !range_bad) m = (int)rintf(__fdiv_rn(row[i], s)) - o;
+    out[(size_t)t * cin + ci] = (int8_t)m;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host twin (native C++, same arithmetic)
+// ------------------------------------------------------------------------------------------
+static int quantize_row_host(float* row, int k, int b, float* s_out) {
+  float mn = INFINITY, mx = -INFINITY;
+  for (int i = 0; i < k; ++i) {
+    mn = std::fmin(mn, row[i]);
+    mx = std::fmax(mx, row[i]);
+  }
+  if (mx == mn) return SMPQ_E_CONSTANT;
+  const double scale = ((double)mx - (double)mn) / (double)((1 << b) - 1);
+  const double zd = std::nearbyint((double)mn / scale) + 0.0;
+  const float s32 = (float)scale;
+  const float z32 = (float)zd;
+  for (int i = 0; i < k; ++i) {
+    const float d = row[i] / s32;  // fp32 IEEE division (contraction is off in this file)
+    const float q = std::nearbyintf(d + z32) - z32;
+    row[i] = q * s32;
+  }
+  *s_out = s32;
+  return SMPQ_OK;
+}
+
+}  // namespace smpq
+
+using namespace smpq;
+
+extern "C" int smpq_quantize_channels(float* w, int cout, int k_elems, const int8_t* bits,
+                                      float* scale_out, int32_t* status, smpq_stream_t stream) {
+  if (!w || !bits || !scale_out || !status || cout <= 0 || k_elems <= 0)
+    return fail(SMPQ_E_INVALID, "smpq_quantize_channels: bad arguments");
+  hipLaunchKernelGGL(quantize_channels_kernel, dim3(cout), dim3(kQThreads), 0,
+                     (hipStream_t)stream, w, k_elems, bits, scale_out, status);
+  return check_hip(hipGetLastError(), "quantize_channels_kernel launch");
+}
+
+extern "C" int smpq_quantize_channels_host(float* w, int cout, int k_elems, const int8_t* bits,
+                                           float* scale_out) {
+  if (!w || !bits || cout <= 0 || k_elems <= 0)
+    return fail(SMPQ_E_INVALID, "smpq_quantize_channels_host: bad arguments");
+  for (int c = 0; c < cout; ++c) {
+    const int b = bits[c];
+    if (b <= 0) continue;
+    if (b > 30) return fail(SMPQ_E_BITS, "smpq_quantize_channels_host: bit > 30");
+    float* row = w + (size_t)c * k_elems;
+    float s32 = 0.f;
+    const int rc = quantize_row_host(row, k_elems, b, &s32);
+    if (rc != SMPQ_OK)
+      return fail(rc, "float division by zero (constant channel " + std::to_string(c) + ")");
+    if (scale_out) scale_out[c] = s32;
+  }
+  return SMPQ_OK;
+}
+
+extern "C" int smpq_pack_weights(const float* w, int cout, int cin, int kh, int kw,
+                                 const float* step, int8_t* codes, int32_t* offset,
+                                 int32_t* status, smpq_stream_t stream) {
+  if (!w || !step || !codes || !offset || !status || cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0)
+    return fail(SMPQ_E_INVALID, "smpq_pack_weights: bad arguments");
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(cout), dim3(kQThreads), 0, (hipStream_t)stream, w,
+                     cin, kh, kw, step, codes, offset, status);
+  return check_hip(hipGetLastError(), "pack_weights_kernel launch");
+}

@@ -1,0 +1,151 @@
+"""Tensor-level wrappers over the libsmpq C-ABI (include/smpq.h).
+
+Every function validates shapes/dtypes/devices on the host before launching, so a kernel
+never sees an operand that disagrees with its grid (no device-side faults on bad input).
+"""
+import torch
+
+from . import _lib
+
+# activation code width in int8 limbs (1 = int8, 2 = int16, 3 = int24); see DESIGN.md
+_ACT_LIMBS = [2]
+# optional launch observer (bench.py): object with begin() / end(alg_ops, shape) around each conv
+_CONV_HOOK = [None]
+LIMB_QMAX = {1: 127.0, 2: 32512.0, 3: 8323072.0}
+
+
+def set_act_limbs(limbs):
+    if limbs not in (1, 2, 3):
+        raise ValueError("act limbs must be 1, 2 or 3")
+    _ACT_LIMBS[0] = int(limbs)
+
+
+def get_act_limbs():
+    return _ACT_LIMBS[0]
+
+
+def _req(cond, msg):
+    if not cond:
+        raise ValueError("smpq: " + msg)
+
+
+def quantize_channels_(w2d, bits):
+    """In-place fake-quantization of the rows of ``w2d`` (functions.py:25-43 per channel).
+
+    w2d: fp32 [cout, k] contiguous (CPU or GPU); bits: int sequence/tensor [cout], 0 = skip.
+    Returns the fp32 step (fp32(scale)) per row (0 for skipped rows) on w2d's device.
+    Raises ZeroDivisionError on a constant channel, like the reference (functions.py:40).
+    """
+    _req(w2d.dtype == torch.float32 and w2d.dim() == 2 and w2d.is_contiguous(),
+         "quantize_channels_: need a contiguous fp32 [cout, k] tensor")
+    cout, k = w2d.shape
+    lib = _lib.load()
+    bits_t = torch.as_tensor(bits, dtype=torch.int8).reshape(-1)
+    _req(bits_t.numel() == cout, "quantize_channels_: bits length != cout")
+    _req(bool((bits_t >= 0).all()) and bool((bits_t <= 16).all()), "bits outside [0, 16]")
+    if w2d.is_cuda:
+        bits_d = bits_t.to(w2d.device)
+        step = torch.zeros(cout, dtype=torch.float32, device=w2d.device)
+        status = torch.zeros(1, dtype=torch.int32, device=w2d.device)
+        with torch.cuda.device(w2d.device):
+            _lib.check(lib.smpq_quantize_channels(_lib.ptr(w2d), cout, k, _lib.ptr(bits_d),
+                                                  _lib.ptr(step), _lib.ptr(status),
+                                                  _lib.stream_ptr()), "smpq_quantize_channels")
+        bad = int(status.item())  # one sync: the reference raises synchronously
+        if bad:
+            raise ZeroDivisionError("float division by zero (constant channel %d)" % (bad - 1))
+        return step
+    step = torch.zeros(cout, dtype=torch.float32)
+    bits_c = bits_t.contiguous()
+    rc = lib.smpq_quantize_channels_host(_lib.ptr(w2d), cout, k, _lib.ptr(bits_c), _lib.ptr(step))
+    if rc == _lib.SMPQ_E_CONSTANT:
+        raise ZeroDivisionError(_lib.last_error())
+    _lib.check(rc, "smpq_quantize_channels_host")
+    return step
+
+
+def pack_weights(w, step):
+    """fp32 fake-quantized weight [cout, cin, kh, kw] -> (codes int8 [cout, kh*kw*cin], offset int32)."""
+    _req(w.is_cuda and w.dtype == torch.float32 and w.dim() == 4, "pack_weights: need a CUDA fp32 4-D weight")
+    w = w.contiguous()
+    cout, cin, kh, kw = w.shape
+    step = step.to(device=w.device, dtype=torch.float32).contiguous()
+    _req(step.numel() == cout, "pack_weights: step length")
+    codes = torch.empty(cout, kh * kw * cin, dtype=torch.int8, device=w.device)
+    offset = torch.empty(cout, dtype=torch.int32, device=w.device)
+    status = torch.zeros(2, dtype=torch.int32, device=w.device)
+    lib = _lib.load()
+    with torch.cuda.device(w.device):
+        _lib.check(lib.smpq_pack_weights(_lib.ptr(w), cout, cin, kh, kw, _lib.ptr(step), _lib.ptr(codes),
+                                         _lib.ptr(offset), _lib.ptr(status), _lib.stream_ptr()),
+                   "smpq_pack_weights")
+    return codes, offset, status
+
+
+def act_absmax(x_nhwc, out=None):
+    """Per-image max|x| of an NHWC (or any [n, ...]) fp32 CUDA tensor -> fp32 [n]."""
+    _req(x_nhwc.is_cuda and x_nhwc.dtype == torch.float32 and x_nhwc.is_contiguous(),
+         "act_absmax: need a contiguous CUDA fp32 tensor")
+    n = x_nhwc.shape[0]
+    if out is None:
+        out = torch.zeros(n, dtype=torch.float32, device=x_nhwc.device)
+    _req(out.numel() == n and out.dtype == torch.float32 and out.is_contiguous(), "act_absmax: out")
+    per = x_nhwc.numel() // n
+    lib = _lib.load()
+    with torch.cuda.device(x_nhwc.device):
+        _lib.check(lib.smpq_act_absmax(_lib.ptr(x_nhwc), n, per, _lib.ptr(out), _lib.stream_ptr()),
+                   "smpq_act_absmax")
+    return out
+
+
+def conv2d_nhwc(x, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
+                residual=None, relu=False, limbs=None, y_absmax=None, out=None):
+    """Quantized conv on NHWC fp32: y = conv(x, codes) * s_x * col_scale + col_shift (+res) (relu)."""
+    limbs = limbs or get_act_limbs()
+    _req(x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous(), "conv: x must be NHWC fp32 CUDA")
+    n, h, w, cin = x.shape
+    cout = codes.shape[0]
+    _req(codes.dtype == torch.int8 and codes.shape == (cout, kh * kw * cin) and codes.is_contiguous(), "conv: codes shape")
+    _req(cin % 64 == 0, "conv: cin must be a multiple of 64")
+    _req(offset is None or (offset.dtype == torch.int32 and offset.numel() == cout), "conv: offset")
+    _req(x_absmax.dtype == torch.float32 and x_absmax.numel() == n, "conv: x_absmax")
+    for t in (col_scale, col_shift):
+        _req(t.dtype == torch.float32 and t.numel() == cout and t.is_contiguous() and t.device == x.device, "conv: col vectors")
+    ho = (h + 2 * pad - kh) // stride + 1
+    wo = (w + 2 * pad - kw) // stride + 1
+    if out is None:
+        out = torch.empty(n, ho, wo, cout, dtype=torch.float32, device=x.device)
+    _req(out.shape == (n, ho, wo, cout) and out.is_contiguous(), "conv: out shape")
+    if residual is not None:
+        _req(residual.shape == (n, ho, wo, cout) and residual.is_contiguous() and residual.dtype == torch.float32,
+             "conv: residual shape")
+    if y_absmax is not None:
+        _req(y_absmax.numel() == n and y_absmax.dtype == torch.float32, "conv: y_absmax")
+    lib = _lib.load()
+    hook = _CONV_HOOK[0]
+    if hook is not None:
+        hook.begin()
+    with torch.cuda.device(x.device):
+        _lib.check(lib.smpq_conv2d_fwd(
+            _lib.ptr(x), _lib.ptr(x_absmax), n, h, w, cin, _lib.ptr(codes), _lib.ptr(offset), cout, kh, kw,
+            stride, pad, _lib.ptr(col_scale), _lib.ptr(col_shift), _lib.ptr(residual), 1 if relu else 0,
+            int(limbs), _lib.ptr(out), _lib.ptr(y_absmax), _lib.stream_ptr()), "smpq_conv2d_fwd")
+    if hook is not None:
+        hook.end(2 * n * ho * wo * cout * kh * kw * cin, (n, h, w, cin, cout, kh, stride))
+    return out
+
+
+def set_conv_hook(hook):
+    _CONV_HOOK[0] = hook
+
+
+def debug_mfma_i8(a, b):
+    """One v_mfma_i32_16x16x64_i8 with the kernel's fragment mapping: a[16,64] @ b[16,64]^T."""
+    _req(a.is_cuda and a.dtype == torch.int8 and a.shape == (16, 64), "debug_mfma: a")
+    _req(b.is_cuda and b.dtype == torch.int8 and b.shape == (16, 64), "debug_mfma: b")
+    c = torch.empty(16, 16, dtype=torch.int32, device=a.device)
+    lib = _lib.load()
+    with torch.cuda.device(a.device):
+        _lib.check(lib.smpq_debug_mfma_i8(_lib.ptr(a.contiguous()), _lib.ptr(b.contiguous()), _lib.ptr(c),
+                                          _lib.stream_ptr()), "smpq_debug_mfma_i8")
+    return c

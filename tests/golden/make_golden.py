@@ -1,0 +1,326 @@
+"""Generate golden fixtures by importing the reference itself (CPU, build container only).
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+Writes (all data, no reference source):
+  tests/golden/quant_kat.npz          quantize_wgt known-answer vectors (functions.py:25-43)
+  tests/golden/model_goldens.npz      logits of seeded reference models on seeded inputs,
+                                      per-conv weight checksums, BN state of the parity models
+  <pkg>/smpq/data/assign_*.npz        per-channel bit/chain assignments for the bench configs
+                                      (R50 reconstruction: SURVEY.md Appendix B)
+
+The reference is imported from /root/reference with a stub ``imagenet`` module
+(the real one needs torchvision and ./hogehoge, imagenet.py:7-40). Pretrained weights
+are a network fetch (resnet.py:15-19) and are not used: models are the reference's own
+``pretrained=False`` init under ``torch.manual_seed``.
+"""
+import csv
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+PKG_DATA = os.path.join(REPO, "semilayer-wise-mixed-precision-quantization_amd", "smpq", "data")
+
+
+def import_reference():
+    sys.path.insert(0, REF)
+    stub = types.ModuleType("imagenet")
+    stub.val_loader = None
+    sys.modules["imagenet"] = stub
+    import functions  # noqa: E402
+    import resnet  # noqa: E402
+    return functions, resnet
+
+
+# ----------------------------------------------------------------------------------------
+# Bit assignments
+# ----------------------------------------------------------------------------------------
+
+R50_LAYERS = [3, 4, 6, 3]
+
+
+def r50_numel_per_channel():
+    """lnum (1..48) -> Cin*k*k of that conv (resnet.py:80-95, _make_layer :181-202)."""
+    numel = {}
+    lnum = 1
+    inplanes = 64
+    for li, nblk in enumerate(R50_LAYERS):
+        planes = 64 * 2 ** li
+        for b in range(nblk):
+            numel[lnum] = inplanes          # conv1 1x1
+            numel[lnum + 1] = planes * 9    # conv2 3x3
+            numel[lnum + 2] = planes        # conv3 1x1
+            lnum += 3
+            inplanes = planes * 4
+    return numel
+
+
+def read_rows(path):
+    with open(path, encoding="utf-8-sig") as f:
+        return list(csv.reader(f))
+
+
+def reconstruct_r50_mixed():
+    """replay resnet50_main.py:155-465 bookkeeping on the CSVs."""
+    rows = read_rows(os.path.join(REF, "dataset", "resnet50_deltaloss.csv"))
+    lnum = np.array([int(v) for v in rows[0]])
+    cnum = np.array([int(v) - 1 for v in rows[1]])
+    delta = {8: np.array([float(v) for v in rows[2]]),
+             6: np.array([float(v) for v in rows[3]]),
+             4: np.array([float(v) for v in rows[4]])}
+    n = len(lnum)
+    numel = r50_numel_per_channel()
+    ne = np.array([numel[l] for l in lnum], dtype=np.float64)
+
+    trace = read_rows(os.path.join(REF, "output", "resnet50ImageNetq864bit_mixedprecision_accs.csv"))
+    cum = [float(v) for v in trace[0]]
+    bits = [int(v) for v in trace[3]]
+    flags = [int(v) for v in trace[4]]
+    lnums = [int(v) for v in trace[5]]
+    counts = [int(v) for v in trace[6]]
+
+    selected = np.full(n, 32, dtype=np.int64)
+    chain = [[] for _ in range(n)]
+    params = 0.0
+    # phases 8 -> 6 -> 4: semilayer = (lnum, delta_b <= 0) over all channels (functions.py:171-177)
+    for col in range(1, len(bits)):
+        if flags[col] != 0:
+            continue
+        b = bits[col]
+        minus = delta[b] <= 0
+        cands = []
+        for sign in (True, False):
+            members = np.nonzero((lnum == lnums[col]) & (minus == sign))[0]
+            if len(members) == counts[col]:
+                cands.append(members)
+        assert len(cands) == 1, ("ambiguous/unmatched accepted semilayer", col, len(cands))
+        members = cands[0]
+        param = float(np.sum(ne[members] * ((32 - b) / 32 - (32 - selected[members]) / 32)))
+        params += param
+        assert abs(params - cum[col]) < 0.5, (col, params, cum[col])
+        for m in members:
+            chain[m].append(b)
+        selected[members] = b
+    # postponing phase (resnet50_main.py:409-465): candidates never accepted, all -> 6-bit.
+    cand = np.nonzero(selected == 32)[0]
+    # reference indexing bug: subset position p is classified by delta6 of FULL-list position p
+    # (functions.py:171-173 fed valuationnexts with the full valuationds at resnet50_main.py:417)
+    minus = delta[6][: len(cand)] <= 0
+    groups = {}
+    for p, m in enumerate(cand):
+        groups.setdefault((int(lnum[m]), bool(minus[p])), []).append(m)
+    published = sorted((lnums[c], counts[c]) for c in range(1, len(bits)) if flags[c] == 1)
+    mine = sorted((k[0], len(v)) for k, v in groups.items())
+    assert published == mine, "postponing semilayers do not match the published trace"
+    for m in cand:
+        params += ne[m] * ((32 - 6) / 32)
+        chain[m].append(6)
+    selected[cand] = 6
+    assert abs(params - cum[-1]) < 0.5, (params, cum[-1])
+    assert int(round(params)) == 16622232
+    return lnum, cnum, chain
+
+
+def r18_uniform8():
+    rows = read_rows(os.path.join(REF, "dataset", "resnet18_deltaloss.csv"))
+    lnum = np.array([int(v) for v in rows[0] if v != ""])
+    cnum = np.array([int(v) - 1 for v in rows[1] if v != ""])
+    return lnum, cnum, [[8] for _ in range(len(lnum))]
+
+
+def r34_4bit_dominant():
+    """b=4 if d4 <= p75(d4), else 6 if d6 <= 0, else 8."""
+    rows = read_rows(os.path.join(REF, "dataset", "resnet34_deltaloss.csv"))
+    lnum = np.array([int(v) for v in rows[0]])
+    cnum = np.array([int(v) - 1 for v in rows[1]])
+    d6 = np.array([float(v) for v in rows[3]])
+    d4 = np.array([float(v) for v in rows[4]])
+    p75 = np.percentile(d4, 75)
+    b = np.where(d4 <= p75, 4, np.where(d6 <= 0, 6, 8))
+    return lnum, cnum, [[int(x)] for x in b]
+
+
+def save_assignment(name, arch, lnum, cnum, chain):
+    c = np.zeros((len(chain), 3), dtype=np.int8)
+    for i, ch in enumerate(chain):
+        c[i, : len(ch)] = ch
+    path = os.path.join(PKG_DATA, "assign_%s.npz" % name)
+    np.savez_compressed(path, arch=np.array(arch), lnum=lnum.astype(np.int16),
+                        cnum=cnum.astype(np.int16), chain=c)
+    hist = {}
+    for ch in chain:
+        hist[tuple(ch)] = hist.get(tuple(ch), 0) + 1
+    print("assignment", name, arch, len(chain), hist)
+    return c
+
+
+# ----------------------------------------------------------------------------------------
+# Quantizer KATs
+# ----------------------------------------------------------------------------------------
+
+def make_quant_kat(functions, resnet):
+    ins, outs, bitl, offs, kinds = [], [], [], [0], []
+
+    def add(t, chain, kind):
+        t = t.detach().clone().float().contiguous()
+        x = t.clone()
+        for b in chain:
+            x = functions.quantize_wgt(x, b)
+        ins.append(t.numpy().ravel())
+        outs.append(x.numpy().ravel())
+        cb = np.zeros(3, dtype=np.int8)
+        cb[: len(chain)] = chain
+        bitl.append(cb)
+        offs.append(offs[-1] + t.numel())
+        kinds.append(kind)
+
+    g = torch.Generator().manual_seed(1234)
+    for size in (9, 64, 576, 1152, 4608):
+        for b in (8, 6, 4, 2):
+            for s in range(2):
+                add(torch.randn(size, generator=g) * 0.05, [b], "randn")
+    add(torch.tensor([-1.0, -0.5, 0.0, 0.5, 1.0, 0.3]), [2], "tie")
+    # realistic channels from the seeded reference model (kaiming fan_out init, resnet.py:165-167)
+    torch.manual_seed(0)
+    net = resnet.resnet18()
+    w = net.layer2[0].conv1.weight.data
+    for i in range(4):
+        for b in (8, 6, 4, 2):
+            add(w[i].reshape(-1), [b], "kaiming")
+    for chain in ([8, 4], [6, 4], [8, 6], [8, 6, 4], [4, 4], [8, 8]):
+        add(w[5].reshape(-1), chain, "chain")
+    # channels where the +z/-z of functions.py:41 changes the result vs round(t/s)
+    found = 0
+    gz = torch.Generator().manual_seed(99)
+    while found < 6:
+        t = torch.randn(576, generator=gz) * 0.03 + 0.01
+        for b in (8, 6, 4, 2):
+            mn, mx = t.min().item(), t.max().item()
+            s = (mx - mn) / (2 ** b - 1)
+            plain = (t / s).round() * s
+            if not torch.equal(plain, functions.quantize_wgt(t, b)):
+                add(t, [b], "zmatters")
+                found += 1
+    # constant channel raises ZeroDivisionError in the reference
+    try:
+        functions.quantize_wgt(torch.full((9,), 0.25), 8)
+        raised = False
+    except ZeroDivisionError:
+        raised = True
+    assert raised
+    np.savez_compressed(os.path.join(HERE, "quant_kat.npz"), x=np.concatenate(ins),
+                        y=np.concatenate(outs), chain=np.stack(bitl),
+                        offsets=np.array(offs, dtype=np.int64), kinds=np.array(kinds),
+                        const_raises=np.array(raised))
+    print("quant KAT cases:", len(kinds))
+
+
+# ----------------------------------------------------------------------------------------
+# Model goldens
+# ----------------------------------------------------------------------------------------
+
+ARCH_MAP = {"resnet18": ("basic", [2, 2, 2, 2]), "resnet34": ("basic", [3, 4, 6, 3]),
+            "resnet50": ("bottleneck", [3, 4, 6, 3])}
+
+
+def conv_for_lnum(net, arch, lnum):
+    kind, layers = ARCH_MAP[arch]
+    blocks = [blk for L in (net.layer1, net.layer2, net.layer3, net.layer4) for blk in L]
+    if kind == "bottleneck":
+        blk = blocks[(lnum - 1) // 3]
+        return [blk.conv1, blk.conv2, blk.conv3][(lnum - 1) % 3]
+    blk = blocks[(lnum - 1) // 2]
+    return blk.conv1 if lnum % 2 == 1 else blk.conv2
+
+
+def apply_assignment(functions, net, arch, lnum, cnum, chain):
+    """Same per-channel calls the search drivers make (e.g. resnet50_main.py:189-197)."""
+    maxlen = max(len(c) for c in chain)
+    for step in range(maxlen):
+        for i in range(len(lnum)):
+            if step < len(chain[i]):
+                conv = conv_for_lnum(net, arch, int(lnum[i]))
+                conv.weight.data = functions.channel_wise_quantizationperchan(
+                    conv.weight.data, chain[i][step], int(cnum[i]))
+
+
+def bn_recalibrate(net, seed_affine=2, seed_data=3, passes=2, batch=64):
+    """Parity variant: random BN affine + train-mode stat recalibration."""
+    g = torch.Generator().manual_seed(seed_affine)
+    for m in net.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.weight.data = torch.rand(m.weight.shape, generator=g) * 0.5 + 0.75
+            m.bias.data = torch.randn(m.bias.shape, generator=g) * 0.1
+            m.momentum = None
+            m.reset_running_stats()
+    net.train()
+    g3 = torch.Generator().manual_seed(seed_data)
+    with torch.no_grad():
+        for _ in range(passes):
+            net(torch.randn(batch, 3, 224, 224, generator=g3))
+    net.eval()
+    for m in net.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.momentum = 0.1
+
+
+def make_model_goldens(functions, resnet, assigns):
+    out = {}
+    torch.set_num_threads(os.cpu_count())
+    cases = [
+        # name, arch, assignment, batch, recalibrate
+        ("r18_fp32", "resnet18", None, 2, False),
+        ("r18_u8", "resnet18", "r18_u8", 2, False),
+        ("r50_mixed", "resnet50", "r50_mixed", 2, False),
+        ("r34_4bit", "resnet34", "r34_4bit", 2, False),
+        ("r18_u8_cal", "resnet18", "r18_u8", 16, True),
+        ("r50_mixed_cal", "resnet50", "r50_mixed", 8, True),
+    ]
+    for name, arch, aname, batch, cal in cases:
+        torch.manual_seed(0)
+        net = getattr(resnet, arch)(pretrained=False)
+        net.eval()
+        sd0 = net.state_dict()
+        for k, v in sd0.items():
+            if k.endswith("weight") and v.dim() == 4:
+                out["%s/wsum/%s" % (name, k)] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+        if aname is not None:
+            lnum, cnum, chain = assigns[aname]
+            apply_assignment(functions, net, arch, lnum, cnum, chain)
+        if cal:
+            bn_recalibrate(net)
+            for k, v in net.state_dict().items():
+                if ("bn" in k or "downsample.1" in k) and not k.endswith("num_batches_tracked"):
+                    out["%s/bn/%s" % (name, k)] = v.numpy().copy()
+        for k, v in net.state_dict().items():
+            if k.endswith("weight") and v.dim() == 4:
+                out["%s/qsum/%s" % (name, k)] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+        x = torch.randn(batch, 3, 224, 224, generator=torch.Generator().manual_seed(1))
+        out["%s/xsum" % name] = np.array([x.double().sum().item(), x.double().abs().sum().item()])
+        with torch.no_grad():
+            logits = net(x)
+        out["%s/logits" % name] = logits.numpy()
+        print(name, "logits", tuple(logits.shape), "top1", logits.argmax(1)[:8].tolist())
+    np.savez_compressed(os.path.join(HERE, "model_goldens.npz"), **out)
+
+
+def main():
+    os.makedirs(PKG_DATA, exist_ok=True)
+    functions, resnet = import_reference()
+    assigns = {"r50_mixed": reconstruct_r50_mixed(), "r18_u8": r18_uniform8(),
+               "r34_4bit": r34_4bit_dominant()}
+    save_assignment("r50_mixed", "resnet50", *assigns["r50_mixed"])
+    save_assignment("r18_u8", "resnet18", *assigns["r18_u8"])
+    save_assignment("r34_4bit", "resnet34", *assigns["r34_4bit"])
+    make_quant_kat(functions, resnet)
+    make_model_goldens(functions, resnet, assigns)
+
+
+if __name__ == "__main__":
+    main()

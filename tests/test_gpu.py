@@ -1,0 +1,304 @@
+"""GPU parity tests (run on the MI355X box with -m gpu). Every call goes through libsmpq's C-ABI.
+
+Conv-level parity has two checks per case:
+  * vs an exact emulation of the integer path (same activation codes, int GEMM in float64,
+    which is exact for |sum| < 2^53): differences only from the fp32 epilogue, bound 2e-6
+    relative to the magnitude of the terms;
+  * vs the float64 oracle conv on the unquantized activations: bounded by the activation
+    quantization error 0.5 * s_x * sum|w| per output (+ fp32 noise).
+Model-level parity: logits of the fused HIP forward vs the reference's CPU logits (goldens
+from the reference itself), top-1 identical; tolerance per activation width.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+LIMB_QMAX = {1: 127.0, 2: 32512.0, 3: 8323072.0}
+# max |logit - reference logit| / max |reference logit| accepted per activation width
+LOGIT_RTOL = {1: 0.35, 2: 1.5e-2, 3: 2e-4}
+
+
+# ----------------------------------------------------------------------------------------------
+def test_mfma_i8_fragment_mapping(gpu):
+    from smpq import ops
+    g = torch.Generator().manual_seed(0)
+    a = torch.randint(-128, 128, (16, 64), generator=g, dtype=torch.int8)
+    b = torch.randint(-128, 128, (16, 64), generator=g, dtype=torch.int8)
+    c = ops.debug_mfma_i8(a.to(gpu), b.to(gpu)).cpu().numpy()
+    ref = a.numpy().astype(np.int64) @ b.numpy().astype(np.int64).T
+    np.testing.assert_array_equal(c, ref)
+
+
+def test_device_quantizer_bitexact_vs_reference(gpu):
+    from smpq import ops
+    from test_oracle_golden import kat_cases
+    for kind, chain, x, y in kat_cases():
+        w = torch.from_numpy(x.copy()).reshape(1, -1).to(gpu)
+        for b in chain:
+            ops.quantize_channels_(w, [b])
+        assert np.array_equal(w.cpu().numpy().ravel().view(np.uint32), y.view(np.uint32)), (kind, chain)
+    with pytest.raises(ZeroDivisionError):
+        ops.quantize_channels_(torch.full((1, 9), 0.25, device=gpu), [8])
+
+
+def test_device_quantizer_layer_matches_host(gpu):
+    from smpq import ops
+    g = torch.Generator().manual_seed(5)
+    w = torch.randn(300, 576, generator=g) * 0.05
+    bits = torch.randint(0, 5, (300,), generator=g) * 2  # 0 (skip), 2, 4, 6, 8
+    wd = w.clone().to(gpu)
+    sd = ops.quantize_channels_(wd, bits)
+    wh = w.clone()
+    sh = ops.quantize_channels_(wh, bits)
+    assert torch.equal(wd.cpu().view(torch.int32), wh.view(torch.int32))
+    assert torch.equal(sd.cpu(), sh)
+
+
+# ----------------------------------------------------------------------------------------------
+def make_layer(gpu, cin, cout, k, seed, bits_choice=(8, 6, 4)):
+    from smpq import ops
+    g = torch.Generator().manual_seed(seed)
+    w = (torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cout * k * k)) ** 0.5)
+    bits = torch.tensor(bits_choice)[torch.randint(0, len(bits_choice), (cout,), generator=g)]
+    wd = w.to(gpu).contiguous()
+    step = ops.quantize_channels_(wd.reshape(cout, -1), bits)
+    codes, offset, status = ops.pack_weights(wd, step)
+    assert status.cpu().tolist() == [0, 0]
+    return wd, step, codes, offset
+
+
+def im2col_nhwc(x, k, stride, pad):
+    n, h, w, c = x.shape
+    xp = np.pad(x, ((0, 0), (pad, pad), (pad, pad), (0, 0)))
+    ho = (h + 2 * pad - k) // stride + 1
+    wo = (w + 2 * pad - k) // stride + 1
+    cols = np.empty((n, ho, wo, k, k, c), dtype=x.dtype)
+    for r in range(k):
+        for q in range(k):
+            cols[:, :, :, r, q, :] = xp[:, r:r + stride * ho:stride, q:q + stride * wo:stride, :]
+    return cols.reshape(n * ho * wo, k * k * c), ho, wo
+
+
+def emulate(x, absmax, m_full, kh, stride, pad, col_scale, col_shift, residual, relu, limbs):
+    """Exact emulation of the kernel's integer path (float64 GEMM of int values is exact here)."""
+    qmax = np.float32(LIMB_QMAX[limbs])
+    n = x.shape[0]
+    with np.errstate(divide="ignore"):
+        inv = np.where(absmax > 0, qmax / absmax.astype(np.float32), np.float32(0)).astype(np.float32)
+    q = np.rint((x * inv[:, None, None, None]).astype(np.float32))
+    q = np.clip(q, -qmax, qmax).astype(np.int64)
+    digits = []
+    for _ in range(limbs - 1):
+        lo = ((q + 128) & 255) - 128
+        digits.append(lo)
+        q = (q - lo) >> 8
+    digits.append(q)
+    terms = []
+    for l, d in enumerate(digits):
+        cols, ho, wo = im2col_nhwc(d.astype(np.float64), kh, stride, pad)
+        terms.append(cols @ m_full.T.astype(np.float64) * (256.0 ** l))
+    v = sum(terms)
+    mag = sum(np.abs(t) for t in terms)
+    rscale = (absmax.astype(np.float32) * np.float32(1.0 / LIMB_QMAX[limbs])).astype(np.float64)
+    rs = np.repeat(rscale, ho * wo)[:, None]
+    y = v * rs * col_scale[None, :] + col_shift[None, :]
+    bound = mag * rs * np.abs(col_scale[None, :]) + np.abs(col_shift[None, :])
+    if residual is not None:
+        y = y + residual.reshape(y.shape)
+        bound = bound + np.abs(residual.reshape(y.shape))
+    if relu:
+        y = np.maximum(y, 0)
+    return y.reshape(n, ho, wo, -1), bound.reshape(n, ho, wo, -1)
+
+
+R18_SHAPES = [(64, 64, 3, 1, 56), (64, 128, 3, 2, 56), (128, 128, 3, 1, 28), (128, 256, 3, 2, 28),
+              (256, 256, 3, 1, 14), (256, 512, 3, 2, 14), (512, 512, 3, 1, 7)]
+R50_SHAPES = [(64, 64, 1, 1, 56), (64, 64, 3, 1, 56), (64, 256, 1, 1, 56), (256, 64, 1, 1, 56),
+              (256, 128, 1, 1, 56), (128, 128, 3, 2, 56), (128, 512, 1, 1, 28), (512, 128, 1, 1, 28),
+              (128, 128, 3, 1, 28), (512, 256, 1, 1, 28), (256, 256, 3, 2, 28), (256, 1024, 1, 1, 14),
+              (1024, 256, 1, 1, 14), (256, 256, 3, 1, 14), (1024, 512, 1, 1, 14), (512, 512, 3, 2, 14),
+              (512, 2048, 1, 1, 7), (2048, 512, 1, 1, 7), (512, 512, 3, 1, 7)]
+EDGE_SHAPES = [(64, 80, 3, 2, 9), (128, 48, 1, 2, 15), (192, 100, 3, 1, 5), (64, 16, 3, 1, 1)]
+
+
+def run_conv_case(gpu, cin, cout, k, stride, hin, limbs, seed, signed=False, residual=False, relu=False, batch=2):
+    from smpq import ops
+    wd, step, codes, offset = make_layer(gpu, cin, cout, k, seed)
+    pad = k // 2
+    g = torch.Generator().manual_seed(seed + 1)
+    x = torch.randn(batch, hin, hin, cin, generator=g)
+    if not signed:
+        x = torch.relu(x)
+    x[min(1, batch - 1)] *= 7.0  # different per-image ranges
+    xd = x.to(gpu)
+    amax = ops.act_absmax(xd)
+    np.testing.assert_array_equal(amax.cpu().numpy(), x.abs().amax(dim=(1, 2, 3)).numpy())
+    col_scale = (step * torch.linspace(0.5, 1.5, cout, device=gpu)).contiguous()
+    col_shift = torch.linspace(-0.1, 0.1, cout, device=gpu).contiguous()
+    ho = (hin + 2 * pad - k) // stride + 1
+    res = torch.randn(batch, ho, ho, cout, generator=g).to(gpu) if residual else None
+    yam = torch.zeros(batch, device=gpu)
+    y = ops.conv2d_nhwc(xd, amax, codes, offset, k, k, stride, pad, col_scale, col_shift,
+                        residual=res, relu=relu, limbs=limbs, y_absmax=yam)
+    torch.cuda.synchronize()
+    yk = y.cpu().numpy().astype(np.float64)
+    # integer-path emulation
+    m_full = (codes.cpu().numpy().astype(np.int64) + offset.cpu().numpy().astype(np.int64)[:, None])
+    ye, bound = emulate(x.numpy(), amax.cpu().numpy(), m_full, k, stride, pad, col_scale.cpu().numpy().astype(np.float64),
+                        col_shift.cpu().numpy().astype(np.float64), None if res is None else res.cpu().numpy().astype(np.float64),
+                        relu, limbs)
+    err = np.abs(yk - ye)
+    assert (err <= 2e-6 * bound + 1e-30).all(), ("emulation mismatch", float((err / (bound + 1e-30)).max()))
+    # fp64 oracle on unquantized activations (conv with the fake-quantized fp32 weights)
+    w_oracle = wd.cpu().numpy().astype(np.float64)  # fl32(m*step): exactly the reference weight
+    wk = w_oracle.transpose(0, 2, 3, 1).reshape(cout, -1)
+    cols, _, _ = im2col_nhwc(x.numpy().astype(np.float64), k, stride, pad)
+    conv = cols @ wk.T
+    cs = (col_scale.cpu().numpy().astype(np.float64) / step.cpu().numpy().astype(np.float64))
+    yt = conv * cs[None, :] + col_shift.cpu().numpy()[None, :]
+    if res is not None:
+        yt = yt + res.cpu().numpy().reshape(yt.shape)
+    if relu:
+        yt = np.maximum(yt, 0)
+    sx = np.repeat(amax.cpu().numpy() / LIMB_QMAX[limbs], ho * ho)[:, None]
+    qbound = 0.5 * sx * (np.abs(cols) > -1).astype(np.float64) @ np.abs(wk).T * np.abs(cs)[None, :] * 1.0001
+    qbound = qbound + 1e-5 * np.abs(yt) + 1e-6
+    assert (np.abs(yk.reshape(yt.shape) - yt) <= qbound).all()
+    # fused absmax output
+    ya = np.abs(yk).reshape(batch, -1).max(1)
+    np.testing.assert_array_equal(yam.cpu().numpy(), ya.astype(np.float32))
+    return offset
+
+
+@pytest.mark.parametrize("shape", R18_SHAPES + R50_SHAPES, ids=lambda s: "c%d_o%d_k%d_s%d_h%d" % s)
+def test_conv_shapes_int16(gpu, shape):
+    cin, cout, k, s, h = shape
+    run_conv_case(gpu, cin, cout, k, s, h, limbs=2, seed=cin + cout + k)
+
+
+@pytest.mark.parametrize("limbs", [1, 2, 3])
+@pytest.mark.parametrize("shape", [(64, 64, 3, 1, 56), (256, 1024, 1, 1, 14), (512, 512, 3, 2, 14)] + EDGE_SHAPES,
+                         ids=lambda s: "c%d_o%d_k%d_s%d_h%d" % s)
+def test_conv_limbs_and_edges(gpu, shape, limbs):
+    cin, cout, k, s, h = shape
+    run_conv_case(gpu, cin, cout, k, s, h, limbs=limbs, seed=7 * cin + cout, signed=True, residual=True, relu=True, batch=3)
+
+
+def test_conv_offsets_exercised(gpu):
+    # 8-bit channels need a code offset whenever their code range is not inside [-128, 127]
+    off = run_conv_case(gpu, 256, 256, 1, 1, 14, limbs=2, seed=3)
+    assert (off != 0).any()
+
+
+# ----------------------------------------------------------------------------------------------
+def _golden():
+    return np.load(os.path.join(GOLDEN, "model_goldens.npz"), allow_pickle=False)
+
+
+def build_model(gpu, arch, assign, cal_case=None):
+    import resnet
+    from smpq import assignments
+    torch.manual_seed(0)
+    net = getattr(resnet, arch)()
+    if cal_case is not None:
+        g = _golden()
+        sd = net.state_dict()
+        pref = cal_case + "/bn/"
+        for k in g.files:
+            if k.startswith(pref):
+                sd[k[len(pref):]].copy_(torch.from_numpy(g[k]))
+    net = net.to(gpu).eval()
+    if assign:
+        assignments.apply_assignment(net, assign)
+    return net
+
+
+@pytest.mark.parametrize("limbs", [2, 3])
+@pytest.mark.parametrize("case,arch,assign,batch", [
+    ("r18_u8", "resnet18", "r18_u8", 2), ("r50_mixed", "resnet50", "r50_mixed", 2),
+    ("r34_4bit", "resnet34", "r34_4bit", 2), ("r18_u8_cal", "resnet18", "r18_u8", 16),
+    ("r50_mixed_cal", "resnet50", "r50_mixed", 8)])
+def test_model_logits_vs_reference(gpu, case, arch, assign, batch, limbs):
+    from smpq import ops, stats
+    g = _golden()
+    net = build_model(gpu, arch, assign, case if case.endswith("_cal") else None)
+    for k in g.files:  # fake-quantized weights identical to the reference's (checksums)
+        if k.startswith(case + "/qsum/"):
+            w = net.state_dict()[k[len(case + "/qsum/"):]].double().cpu()
+            np.testing.assert_allclose([w.sum().item(), w.abs().sum().item()], g[k], rtol=1e-12, atol=1e-12)
+    x = torch.randn(batch, 3, 224, 224, generator=torch.Generator().manual_seed(1))
+    ops.set_act_limbs(limbs)
+    try:
+        before = stats["hip_conv"]
+        with torch.no_grad():
+            y = net(x.to(gpu)).double().cpu().numpy()
+        nq = {"resnet18": 16, "resnet34": 32, "resnet50": 48}[arch]
+        assert stats["hip_conv"] - before == nq
+    finally:
+        ops.set_act_limbs(2)
+    ref = g[case + "/logits"].astype(np.float64)
+    rel = np.abs(y - ref).max() / np.abs(ref).max()
+    assert rel <= LOGIT_RTOL[limbs], rel
+    assert (y.argmax(1) == ref.argmax(1)).all()
+
+
+def test_batch_invariance_and_determinism(gpu):
+    """Per-image activation ranges => each image's logits do not depend on the batch."""
+    net = build_model(gpu, "resnet18", "r18_u8")
+    x = torch.randn(256, 3, 224, 224, generator=torch.Generator().manual_seed(11)).to(gpu)
+    with torch.no_grad():
+        y_big = net(x)
+        y_big2 = net(x)
+        y_small = net(x[100:103].contiguous())
+    assert torch.equal(y_big, y_big2)
+    assert torch.equal(y_big[100:103], y_small)
+
+
+def test_dropin_gpu_quantizer_and_fp32_channels(gpu):
+    import functions
+    from smpq import stats
+    net = build_model(gpu, "resnet18", None)
+    conv = net.layer2[1].conv2
+    for c in range(conv.out_channels - 1):  # leave the last channel unquantized
+        functions.channel_wise_quantizationperchan(conv.weight.data, 6, c)
+    assert conv._bits_host[-1] == 0 and conv.fully_quantized() is False
+    x = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(2)).to(gpu)
+    f0 = stats["fp32_conv"]
+    with torch.no_grad():
+        net(x)
+    assert stats["fp32_conv"] - f0 == 16  # nothing else quantized in this net: all fp32
+    functions.channel_wise_quantizationperchan(conv.weight.data, 6, conv.out_channels - 1)
+    assert conv.fully_quantized()
+    h0 = stats["hip_conv"]
+    with torch.no_grad():
+        net(x)
+    assert stats["hip_conv"] - h0 == 1
+
+
+def test_module_path_matches_fused(gpu):
+    net = build_model(gpu, "resnet50", "r50_mixed")
+    x = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(3)).to(gpu)
+    with torch.no_grad():
+        y_fused = net(x)
+        net.fused = False
+        y_mod = net(x)
+        net.fused = True
+    rel = (y_fused - y_mod).abs().max() / y_mod.abs().max()
+    assert rel < 1.5e-2
+
+
+def test_evaluate_acc_loss_softmax(gpu):
+    import functions
+    import imagenet
+    net = build_model(gpu, "resnet18", "r18_u8")
+    loader = imagenet.SyntheticImageNet(n_images=8, batch_size=4)
+    acc, loss, outs = functions.evaluate_acc_loss_softmax(net, gpu, loader)
+    assert 0.0 <= acc <= 1.0 and np.isfinite(loss) and len(outs) == 2 and outs[0].shape == (4, 1000)
+    torch.testing.assert_close(outs[0].sum(1), torch.ones(4, device=gpu))
+    assert functions.KLdiv(outs, outs) == pytest.approx(0.0, abs=1e-6)

@@ -1,0 +1,87 @@
+"""libsmpq on the host: ABI exports, the native host quantizer vs the reference's KAT vectors,
+and the drop-in functions API on CPU tensors (no GPU needed)."""
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO
+from test_oracle_golden import kat_cases
+
+
+def header_symbols():
+    src = open(REPO + "/include/smpq.h").read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\*\s]+?\b(smpq_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_header_symbol(built_lib):
+    syms = header_symbols()
+    assert len(syms) >= 9
+    from smpq import _lib
+    for s in syms:
+        assert hasattr(built_lib, s), s
+        assert s in _lib.EXPORTED_SYMBOLS, s
+    assert built_lib.smpq_abi_version() == 1
+
+
+def test_host_quantizer_bitexact_vs_reference(built_lib):
+    from smpq import ops
+    for kind, chain, x, y in kat_cases():
+        w = torch.from_numpy(x.copy()).reshape(1, -1)
+        for b in chain:
+            ops.quantize_channels_(w, [b])
+        assert np.array_equal(w.numpy().ravel().view(np.uint32), y.view(np.uint32)), (kind, chain)
+
+
+def test_host_quantizer_constant_channel(built_lib):
+    from smpq import ops
+    w = torch.full((1, 9), 0.25)
+    with pytest.raises(ZeroDivisionError):
+        ops.quantize_channels_(w, [8])
+
+
+def test_dropin_functions_record_metadata(built_lib):
+    import functions
+    import resnet
+    torch.manual_seed(0)
+    net = resnet.resnet18()
+    conv = net.layer1[0].conv1
+    before = conv.weight.data[3].clone()
+    ret = functions.channel_wise_quantizationperchan(conv.weight.data, 6, 3)
+    assert ret.data_ptr() == conv.weight.data_ptr()
+    from oracle import quant_ref
+    exp = quant_ref.quantize_wgt(before.numpy(), 6)
+    assert np.array_equal(conv.weight.data[3].numpy().view(np.uint32), exp.view(np.uint32))
+    assert int(conv.qbits[3]) == 6 and float(conv.qstep[3]) > 0 and conv._bits_host[3] == 6
+    assert int(conv.qbits[2]) == 0
+    # quantize_wgt returns a new tensor and records nothing
+    t = conv.weight.data[5].clone()
+    q = functions.quantize_wgt(t, 4)
+    assert q.data_ptr() != t.data_ptr() and int(conv.qbits[5]) == 0
+    # metadata survives state_dict round trip (resnet50_main.py:212,233-234)
+    sd = net.state_dict()
+    net2 = resnet.resnet18()
+    net2.load_state_dict(sd)
+    assert int(net2.layer1[0].conv1.qbits[3]) == 6 and net2.layer1[0].conv1._bits_host[3] == 6
+
+
+def test_dropin_semilayer_split_and_order():
+    import functions
+    params = [[0, 0, 1, c, 8, 0, 32, c + 1] for c in range(4)] + [[0, 0, 2, c, 8, 0, 32, 5 + c] for c in range(3)]
+    d = [[0, 0, 0, 0, v] for v in (-1, 2, 0, 3, 5, -2, -1)]
+    minus, plus = functions.make_divide_minusplusmodels(params, d, 4)
+    assert [r[3] for r in minus] == [0, 2, 1, 2] and [r[5] for r in minus] == [0, 0, -1, -1]
+    assert [r[3] for r in plus] == [1, 3, 0] and [r[5] for r in plus] == [1, 1, 2]
+    sem = [[params[0]], [params[1], params[3]], [params[4]]]
+    flat = functions.make_quantizedlists(sem, [[0, 0.5], [1, 0.1], [2, 0.3]])
+    assert [r[3] for r in flat[:-1]] == [1, 3, 0, 0] and flat[-1][2] == 100
+
+
+def test_dropin_kldiv_matches_formula():
+    import functions
+    g = torch.Generator().manual_seed(0)
+    p = [torch.softmax(torch.randn(5, 10, generator=g), 1) for _ in range(3)]
+    q = [torch.softmax(torch.randn(5, 10, generator=g), 1) for _ in range(3)]
+    ref = np.mean([float((a[i] * (a[i] / b[i]).log()).sum()) for a, b in zip(p, q) for i in range(5)])
+    assert abs(functions.KLdiv(p, q) - ref) < 1e-6
