@@ -22,6 +22,8 @@
  *                                  BasicBlock.forward (resnet.py:55-68) / Bottleneck.forward
  *                                  (resnet.py:97-116)
  *   smpq_act_absmax                (new) per-image activation range for the activation quantizer
+ *   smpq_act_quantize              (new) activation quantizer (the reference keeps fp32 activations;
+ *                                  int16/int24 codes reproduce them within the stated tolerance)
  */
 #ifndef SMPQ_H_
 #define SMPQ_H_
@@ -79,10 +81,19 @@ int smpq_pack_weights(const float* w, int cout, int cin, int kh, int kw, const f
 int smpq_act_absmax(const float* x, int n, int64_t per_image, float* absmax,
                     smpq_stream_t stream);
 
-/* Quantized conv forward (implicit GEMM on int8 MFMA), NHWC fp32 in/out.
- *   x          device fp32 NHWC [n][h][w][cin]; cin % 64 == 0
- *   x_absmax   device fp32 [n] per-image max|x| (activation quantizer range)
- *   codes/offset/cout/kh/kw: from smpq_pack_weights
+/* Activation quantizer: q = clamp(rne(x * QMAX_L / absmax[img]), +-QMAX_L) with
+ * QMAX_1 = 127, QMAX_2 = 32512, QMAX_3 = 8323072, written as `limbs` balanced base-256 int8
+ * digit planes (q = sum_l 256^l * plane_l), each plane laid out like x.
+ *   x        device fp32, n images of per_image elements (per_image % 8 == 0)
+ *   absmax   device fp32 [n] (from smpq_act_absmax or a conv's y_absmax)
+ *   out      device int8 [limbs][n * per_image] */
+int smpq_act_quantize(const float* x, int n, int64_t per_image, const float* absmax, int limbs,
+                      int8_t* out, smpq_stream_t stream);
+
+/* Quantized conv forward (implicit GEMM on int8 MFMA), NHWC.
+ *   xq         device int8 [limbs][n][h][w][cin] digit planes from smpq_act_quantize; cin % 64 == 0
+ *   x_absmax   device fp32 [n]: the per-image range xq was quantized with
+ *   codes/offset/cout/kh/kw: from smpq_pack_weights (offset may be NULL when all zero)
  *   col_scale  device fp32 [cout]: y = conv_real * col_scale[c] + col_shift[c]
  *              (col_scale = step * bn_gamma / sqrt(var+eps), col_shift = bn_beta - mean * ...)
  *   residual   device fp32 NHWC [n][ho][wo][cout] added after the affine, or NULL
@@ -90,7 +101,7 @@ int smpq_act_absmax(const float* x, int n, int64_t per_image, float* absmax,
  *   limbs      activation code width in int8 limbs: 1 (int8), 2 (int16), 3 (int24)
  *   y          device fp32 NHWC [n][ho][wo][cout]
  *   y_absmax   device fp32 [n] (caller-zeroed), receives max|y| per image, or NULL */
-int smpq_conv2d_fwd(const float* x, const float* x_absmax, int n, int h, int w, int cin,
+int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                     const int8_t* codes, const int32_t* offset, int cout, int kh, int kw,
                     int stride, int pad, const float* col_scale, const float* col_shift,
                     const float* residual, int relu, int limbs, float* y, float* y_absmax,

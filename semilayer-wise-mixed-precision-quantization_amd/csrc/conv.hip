@@ -13,10 +13,12 @@
 // the kernel multiplies the integer code m (exact) and applies `step` once per output, so the
 // only weight-side difference is the <= 2^-24 relative rounding inside fl32(m * step).
 //
-// Activation side: x is quantized ON LOAD with a per-image step s_x = max|x_img| / QMAX into
-// an integer q with `L` balanced base-256 int8 digits (limbs): q = sum_l 256^l d_l.
-// L = 1 gives int8, L = 2 int16, L = 3 int24 fixed point; each limb is one MFMA pass over the
-// same B fragment, accumulated in its own int32 accumulator, recombined in fp32 in the epilogue.
+// Activation side: x is quantized ONCE per element by act_quantize_kernel with a per-image step
+// s_x = max|x_img| / QMAX into an integer q with `L` balanced base-256 int8 digits (limbs),
+// q = sum_l 256^l d_l, stored as L int8 planes (NHWC each). L = 1 gives int8, L = 2 int16,
+// L = 3 int24 fixed point. The GEMM copies limb bytes straight into LDS; each limb is one MFMA
+// pass over the same B fragment, accumulated in its own int32 accumulator and recombined in
+// fp32 in the epilogue. Per-image steps make every image's result independent of the batch.
 //
 // Tile: 256 threads = 4 waves as 2 (M) x 2 (N); each wave owns WM x WN subtiles of 16 x 16
 // computed with v_mfma_i32_16x16x64_i8 (one K step of 64 per MFMA). Block tile
@@ -33,7 +35,8 @@ constexpr int kKStep = 64;      // K per MFMA (i8 16x16x64)
 constexpr int kRowBytes = 80;   // LDS row stride for a 64-byte K slice (+16 B pad vs conflicts)
 
 struct ConvArgs {
-  const float* x;
+  const int8_t* xq;
+  long long plane;
   const float* x_absmax;
   const int8_t* codes;
   const int32_t* w_off;
@@ -45,7 +48,7 @@ struct ConvArgs {
   int n, h, w, cin, cout, kh, kw, stride, pad, ho, wo;
   int M, K, ksteps, cchunks;
   int relu, has_offset;
-  float qmax, inv_qmax;
+  float inv_qmax;
 };
 
 template <int L>
@@ -64,11 +67,19 @@ template <int L, int WM, int WN>
 __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
   constexpr int BM = 32 * WM;
   constexpr int BN = 32 * WN;
-  constexpr int AROWS = BM / 16;  // A rows loaded per thread per K step (16 threads per row)
   constexpr int BROWS = BN / 64;  // B rows loaded per thread per K step (4 threads per row)
 
-  __shared__ __attribute__((aligned(16))) int8_t As[2][L][BM][kRowBytes];
-  __shared__ __attribute__((aligned(16))) int8_t Bs[2][BN][kRowBytes];
+  // one LDS arena: K-loop operand buffers, then (after the loop) the fp32 output tile
+  constexpr int kLoopBytes = 2 * L * BM * kRowBytes + 2 * BN * kRowBytes;
+  constexpr int TS = BN + 4;  // epilogue tile row stride (floats): conflict-free lane writes
+  constexpr int kEpiBytes = BM * TS * 4;
+  constexpr int kArena = kLoopBytes > kEpiBytes ? kLoopBytes : kEpiBytes;
+  __shared__ __attribute__((aligned(16))) int8_t arena[kArena];
+  typedef int8_t ATile[L][BM][kRowBytes];
+  typedef int8_t BTile[BN][kRowBytes];
+  ATile* As = reinterpret_cast<ATile*>(arena);
+  BTile* Bs = reinterpret_cast<BTile*>(arena + 2 * L * BM * kRowBytes);
+  float* tile = reinterpret_cast<float*>(arena);
   __shared__ float s_rowscale[BM];
   __shared__ int s_rowimg[BM];
   __shared__ unsigned int s_rowmax[BM];
@@ -97,15 +108,15 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
     s_rowmax[r] = 0u;
   }
 
-  // ---- per-thread A load rows: input pixel base, top-left tap coordinate, 1/step ---------
-  const int apiece = tid & 15;  // 16-B piece of the 256-B fp32 K slice (4 channels)
-  const int arow0 = tid >> 4;   // rows arow0 + 16*i
-  int a_pix[AROWS];             // n*h*w pixel base, or -1 when the row is past M
-  int a_ih[AROWS], a_iw[AROWS];
-  float a_inv[AROWS];
+  // ---- per-thread A load rows: input pixel base and top-left tap coordinate -----------------
+  constexpr int AR = BM / 64;   // A rows per thread per limb (4 threads x 16 B per 64-B row)
+  const int piece = tid & 3;    // 16-B piece of a 64-B K slice
+  const int row0 = tid >> 2;    // rows row0 + 64*i (A) / row0 + 64*j (B)
+  int a_pix[AR];                // n*h*w pixel base, or -1 when the row is past M
+  int a_ih[AR], a_iw[AR];
 #pragma unroll
-  for (int i = 0; i < AROWS; ++i) {
-    const int m = m0 + arow0 + 16 * i;
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + row0 + 64 * i;
     if (m < a.M) {
       const int img = m / hw_out;
       const int rem = m - img * hw_out;
@@ -114,18 +125,13 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
       a_pix[i] = img * a.h * a.w;
       a_ih[i] = oh * a.stride - a.pad;
       a_iw[i] = ow * a.stride - a.pad;
-      const float am = a.x_absmax[img];
-      a_inv[i] = am > 0.f ? a.qmax / am : 0.f;
     } else {
       a_pix[i] = -1;
       a_ih[i] = a_iw[i] = 0;
-      a_inv[i] = 0.f;
     }
   }
-  const int bpiece = tid & 3;  // 16-B piece of the 64-B int8 K slice
-  const int brow0 = tid >> 2;  // rows brow0 + 64*j
 
-  float4 ra[AROWS];
+  v4i ra[L][AR];
   v4i rb[BROWS];
 
   auto load_global = [&](int ks) {
@@ -134,22 +140,24 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
     const int kr = tap / a.kw;
     const int kc = tap - kr * a.kw;
 #pragma unroll
-    for (int i = 0; i < AROWS; ++i) {
+    for (int i = 0; i < AR; ++i) {
       const int ih = a_ih[i] + kr;
       const int iw = a_iw[i] + kc;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (a_pix[i] >= 0 && (unsigned)ih < (unsigned)a.h && (unsigned)iw < (unsigned)a.w) {
-        const float* p = a.x + ((size_t)(a_pix[i] + ih * a.w + iw) * a.cin + c0 + 4 * apiece);
-        v = *reinterpret_cast<const float4*>(p);
+      const bool ok = a_pix[i] >= 0 && (unsigned)ih < (unsigned)a.h && (unsigned)iw < (unsigned)a.w;
+      const size_t off = ok ? ((size_t)(a_pix[i] + ih * a.w + iw) * a.cin + c0 + 16 * piece) : 0;
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        v4i v = {0, 0, 0, 0};
+        if (ok) v = *reinterpret_cast<const v4i*>(a.xq + l * a.plane + off);
+        ra[l][i] = v;
       }
-      ra[i] = v;
     }
 #pragma unroll
     for (int j = 0; j < BROWS; ++j) {
-      const int col = n0 + brow0 + 64 * j;
+      const int col = n0 + row0 + 64 * j;
       v4i v = {0, 0, 0, 0};
       if (col < a.cout) {
-        v = *reinterpret_cast<const v4i*>(a.codes + (size_t)col * a.K + ks * kKStep + 16 * bpiece);
+        v = *reinterpret_cast<const v4i*>(a.codes + (size_t)col * a.K + ks * kKStep + 16 * piece);
       }
       rb[j] = v;
     }
@@ -157,28 +165,13 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
 
   auto store_lds = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < AROWS; ++i) {
-      const float vals[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
-      int packed[L];
+    for (int l = 0; l < L; ++l)
 #pragma unroll
-      for (int l = 0; l < L; ++l) packed[l] = 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float qf = rintf(vals[e] * a_inv[i]);
-        qf = fminf(fmaxf(qf, -a.qmax), a.qmax);
-        int d[L];
-        split_limbs<L>((int)qf, d);
-#pragma unroll
-        for (int l = 0; l < L; ++l) packed[l] |= (d[l] & 255) << (8 * e);
-      }
-      const int r = arow0 + 16 * i;
-#pragma unroll
-      for (int l = 0; l < L; ++l)
-        *reinterpret_cast<int*>(&As[buf][l][r][4 * apiece]) = packed[l];
-    }
+      for (int i = 0; i < AR; ++i)
+        *reinterpret_cast<v4i*>(&As[buf][l][row0 + 64 * i][16 * piece]) = ra[l][i];
 #pragma unroll
     for (int j = 0; j < BROWS; ++j)
-      *reinterpret_cast<v4i*>(&Bs[buf][brow0 + 64 * j][16 * bpiece]) = rb[j];
+      *reinterpret_cast<v4i*>(&Bs[buf][row0 + 64 * j][16 * piece]) = rb[j];
   };
 
   v4i acc[L][WM][WN];
@@ -257,12 +250,38 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
     coloff[j] = (ok && a.has_offset) ? a.w_off[col] : 0;
   }
 
+  // The K-loop buffers are dead: the arena becomes the [BM][TS] fp32 output tile. All global
+  // traffic of the epilogue is whole 16-B pieces of contiguous output rows (coalesced), and all
+  // residual loads are issued before any output store (vmcnt retires loads and stores in order).
+  constexpr int V4 = BN / 4;  // float4 per tile row
+  const bool vec_ok = (a.cout & 3) == 0;
+  __syncthreads();
+  if (a.residual) {
+    for (int e = tid; e < BM * V4; e += kThreads) {
+      const int r = e / V4, c4 = e - (e / V4) * V4;
+      const int m = m0 + r, col = n0 + 4 * c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m < a.M) {
+        const float* src = a.residual + (size_t)m * a.cout + col;
+        if (vec_ok && col + 3 < a.cout) {
+          v = *reinterpret_cast<const float4*>(src);
+        } else {
+          if (col < a.cout) v.x = src[0];
+          if (col + 1 < a.cout) v.y = src[1];
+          if (col + 2 < a.cout) v.z = src[2];
+          if (col + 3 < a.cout) v.w = src[3];
+        }
+      }
+      *reinterpret_cast<float4*>(&tile[r * TS + 4 * c4]) = v;
+    }
+    __syncthreads();
+  }
+
 #pragma unroll
   for (int i = 0; i < WM; ++i) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int rloc = arow_base + 16 * i + 4 * (lane >> 4) + r;  // C layout: row = 4*(lane>>4)+reg
-      const int m = m0 + rloc;
       const float rscale = s_rowscale[rloc];
       int rsum[L];
 #pragma unroll
@@ -271,7 +290,7 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
       float rmax = 0.f;
 #pragma unroll
       for (int j = 0; j < WN; ++j) {
-        const int col = n0 + bcol_base + 16 * j + frow;
+        const int cloc = bcol_base + 16 * j + frow;
         float v = 0.f;
         float limbw = 1.f;
 #pragma unroll
@@ -281,13 +300,11 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
           limbw *= 256.f;
         }
         float out = v * (rscale * colscale[j]) + colshift[j];
-        if (m < a.M && col < a.cout) {
-          const size_t idx = (size_t)m * a.cout + col;
-          if (a.residual) out += a.residual[idx];
-          if (a.relu) out = fmaxf(out, 0.f);
-          a.y[idx] = out;
-          rmax = fmaxf(rmax, fabsf(out));
-        }
+        float* tp = &tile[rloc * TS + cloc];
+        if (a.residual) out += *tp;
+        if (a.relu) out = fmaxf(out, 0.f);
+        *tp = out;
+        if (n0 + cloc < a.cout) rmax = fmaxf(rmax, fabsf(out));
       }
       if (a.y_absmax) {
         // reduce over the 16 lanes (columns) that share this row
@@ -295,13 +312,28 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
         rmax = fmaxf(rmax, __shfl_xor(rmax, 2, kWave));
         rmax = fmaxf(rmax, __shfl_xor(rmax, 4, kWave));
         rmax = fmaxf(rmax, __shfl_xor(rmax, 8, kWave));
-        if (frow == 0 && m < a.M) atomicMax(&s_rowmax[rloc], __float_as_uint(rmax));
+        if (frow == 0 && m0 + rloc < a.M) atomicMax(&s_rowmax[rloc], __float_as_uint(rmax));
       }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < BM * V4; e += kThreads) {
+    const int r = e / V4, c4 = e - (e / V4) * V4;
+    const int m = m0 + r, col = n0 + 4 * c4;
+    if (m >= a.M || col >= a.cout) continue;
+    const float4 v = *reinterpret_cast<const float4*>(&tile[r * TS + 4 * c4]);
+    float* dst = a.y + (size_t)m * a.cout + col;
+    if (vec_ok && col + 3 < a.cout) {
+      *reinterpret_cast<float4*>(dst) = v;
+    } else {
+      dst[0] = v.x;
+      if (col + 1 < a.cout) dst[1] = v.y;
+      if (col + 2 < a.cout) dst[2] = v.z;
+      if (col + 3 < a.cout) dst[3] = v.w;
     }
   }
 
   if (a.y_absmax) {
-    __syncthreads();
     if (wave == 0) {
       const int img_lo = s_rowimg[0];
       int last = min(BM, a.M - m0) - 1;
@@ -318,6 +350,46 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// x (fp32, any layout, n images of per_image elements) -> L int8 digit planes of
+// q = clamp(rne(x * (QMAX / absmax[img])), +-QMAX). 8 elements per thread: two float4 loads,
+// one 8-byte store per plane.
+template <int L>
+__global__ __launch_bounds__(256) void act_quantize_kernel(const float* __restrict__ x, long long total,
+                                                           long long per_image,
+                                                           const float* __restrict__ absmax, float qmax,
+                                                           int8_t* __restrict__ out, long long plane) {
+  const long long nvec = total / 8;
+  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec;
+       v += (long long)gridDim.x * blockDim.x) {
+    const long long e = v * 8;
+    const int img = (int)(e / per_image);
+    const float am = absmax[img];
+    const float inv = am > 0.f ? qmax / am : 0.f;
+    const float4 x0 = *reinterpret_cast<const float4*>(x + e);
+    const float4 x1 = *reinterpret_cast<const float4*>(x + e + 4);
+    const float vals[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    unsigned int lo[L], hi[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) lo[l] = hi[l] = 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float qf = rintf(vals[k] * inv);
+      qf = fminf(fmaxf(qf, -qmax), qmax);
+      int d[L];
+      split_limbs<L>((int)qf, d);
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        const unsigned int byte = (unsigned int)(d[l] & 255);
+        if (k < 4) lo[l] |= byte << (8 * k);
+        else hi[l] |= byte << (8 * (k - 4));
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+      *reinterpret_cast<uint2*>(out + l * plane + e) = make_uint2(lo[l], hi[l]);
+  }
+}
+
 __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, int64_t per_image,
                                                      float* __restrict__ out) {
   const int img = blockIdx.y;
@@ -363,12 +435,12 @@ static int launch(const ConvArgs& a, hipStream_t stream) {
 
 using namespace smpq;
 
-extern "C" int smpq_conv2d_fwd(const float* x, const float* x_absmax, int n, int h, int w, int cin,
+extern "C" int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                                const int8_t* codes, const int32_t* offset, int cout, int kh, int kw,
                                int stride, int pad, const float* col_scale, const float* col_shift,
                                const float* residual, int relu, int limbs, float* y, float* y_absmax,
                                smpq_stream_t stream) {
-  if (!x || !x_absmax || !codes || !col_scale || !col_shift || !y)
+  if (!xq || !x_absmax || !codes || !col_scale || !col_shift || !y)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: null pointer");
   if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || stride <= 0 ||
       pad < 0)
@@ -377,7 +449,8 @@ extern "C" int smpq_conv2d_fwd(const float* x, const float* x_absmax, int n, int
     return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: cin must be a multiple of 64 (got " +
                                   std::to_string(cin) + ")");
   ConvArgs a;
-  a.x = x;
+  a.xq = xq;
+  a.plane = (long long)n * h * w * cin;
   a.x_absmax = x_absmax;
   a.codes = codes;
   a.w_off = offset;
@@ -399,7 +472,7 @@ extern "C" int smpq_conv2d_fwd(const float* x, const float* x_absmax, int n, int
   a.wo = (w + 2 * pad - kw) / stride + 1;
   if (a.ho <= 0 || a.wo <= 0) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: empty output");
   const long M = (long)n * a.ho * a.wo;
-  if (M > 0x7fffffffL || (long)n * h * w * (long)cin > 0x7fffffffL * 4L)
+  if (M > 0x7fffffffL || a.plane > 0x7fffffffLL * 8 || (long)n * h * w > 0x7fffffffL)
     return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: tensor too large");
   a.M = (int)M;
   a.K = kh * kw * cin;
@@ -410,20 +483,45 @@ extern "C" int smpq_conv2d_fwd(const float* x, const float* x_absmax, int n, int
   hipStream_t s = (hipStream_t)stream;
   switch (limbs) {
     case 1:
-      a.qmax = 127.f;
       a.inv_qmax = 1.f / 127.f;
       return cout <= 64 ? launch<1, 4, 2>(a, s) : launch<1, 4, 4>(a, s);
     case 2:
-      a.qmax = 32512.f;
       a.inv_qmax = 1.f / 32512.f;
-      return launch<2, 4, 2>(a, s);
+      return cout <= 64 ? launch<2, 4, 2>(a, s) : launch<2, 4, 4>(a, s);
     case 3:
-      a.qmax = 8323072.f;
       a.inv_qmax = 1.f / 8323072.f;
       return launch<3, 4, 2>(a, s);
     default:
       return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: limbs must be 1, 2 or 3");
   }
+}
+
+extern "C" int smpq_act_quantize(const float* x, int n, int64_t per_image, const float* absmax, int limbs,
+                                 int8_t* out, smpq_stream_t stream) {
+  if (!x || !absmax || !out || n <= 0 || per_image <= 0)
+    return fail(SMPQ_E_INVALID, "smpq_act_quantize: bad arguments");
+  if (per_image % 8 != 0) return fail(SMPQ_E_SHAPE, "smpq_act_quantize: per_image % 8 != 0");
+  const long long total = (long long)n * per_image;
+  long long blocks = (total / 8 + 255) / 256;
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  hipStream_t s = (hipStream_t)stream;
+  switch (limbs) {
+    case 1:
+      hipLaunchKernelGGL(act_quantize_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, x, total, per_image,
+                         absmax, 127.f, out, total);
+      break;
+    case 2:
+      hipLaunchKernelGGL(act_quantize_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, x, total, per_image,
+                         absmax, 32512.f, out, total);
+      break;
+    case 3:
+      hipLaunchKernelGGL(act_quantize_kernel<3>, dim3((unsigned)blocks), dim3(256), 0, s, x, total, per_image,
+                         absmax, 8323072.f, out, total);
+      break;
+    default:
+      return fail(SMPQ_E_INVALID, "smpq_act_quantize: limbs must be 1, 2 or 3");
+  }
+  return check_hip(hipGetLastError(), "act_quantize_kernel launch");
 }
 
 extern "C" size_t smpq_conv2d_workspace_bytes(int, int, int, int, int, int, int, int, int, int) {

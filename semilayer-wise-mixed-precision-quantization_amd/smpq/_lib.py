@@ -39,6 +39,7 @@ _PROTOS = {
     "smpq_quantize_channels_host": (_i, [_vp, _i, _i, _vp, _vp]),
     "smpq_pack_weights": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "smpq_act_absmax": (_i, [_vp, _i, _i64, _vp, _vp]),
+    "smpq_act_quantize": (_i, [_vp, _i, _i64, _vp, _i, _vp, _vp]),
     "smpq_conv2d_fwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp,
                              _vp, _i, _i, _vp, _vp, _vp]),
     "smpq_conv2d_workspace_bytes": (ctypes.c_size_t, [_i] * 10),

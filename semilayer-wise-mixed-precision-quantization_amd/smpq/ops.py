@@ -98,23 +98,45 @@ def act_absmax(x_nhwc, out=None):
     return out
 
 
-def conv2d_nhwc(x, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
-                residual=None, relu=False, limbs=None, y_absmax=None, out=None):
-    """Quantized conv on NHWC fp32: y = conv(x, codes) * s_x * col_scale + col_shift (+res) (relu)."""
+def act_quantize(x, x_absmax, limbs=None, out=None):
+    """fp32 [n, ...] -> int8 [limbs, n, ...] balanced digit planes (per-image range x_absmax)."""
     limbs = limbs or get_act_limbs()
-    _req(x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous(), "conv: x must be NHWC fp32 CUDA")
-    n, h, w, cin = x.shape
+    _req(x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(), "act_quantize: need contiguous CUDA fp32")
+    n = x.shape[0]
+    per = x.numel() // n
+    _req(per % 8 == 0, "act_quantize: elements per image must be a multiple of 8")
+    _req(x_absmax.dtype == torch.float32 and x_absmax.numel() == n and x_absmax.device == x.device, "act_quantize: absmax")
+    if out is None:
+        out = torch.empty((limbs,) + tuple(x.shape), dtype=torch.int8, device=x.device)
+    _req(out.shape == (limbs,) + tuple(x.shape) and out.dtype == torch.int8 and out.is_contiguous(), "act_quantize: out")
+    lib = _lib.load()
+    with torch.cuda.device(x.device):
+        _lib.check(lib.smpq_act_quantize(_lib.ptr(x), n, per, _lib.ptr(x_absmax), int(limbs), _lib.ptr(out),
+                                         _lib.stream_ptr()), "smpq_act_quantize")
+    return out
+
+
+def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
+             residual=None, relu=False, y_absmax=None, out=None):
+    """Quantized conv on int8 limb planes xq [L, n, h, w, cin] (from act_quantize):
+    y = conv(x, codes) * s_x * col_scale + col_shift (+res) (relu), NHWC fp32."""
+    _req(xq.is_cuda and xq.dtype == torch.int8 and xq.dim() == 5 and xq.is_contiguous(), "conv: xq must be [L,n,h,w,c] int8")
+    limbs, n, h, w, cin = xq.shape
+    _req(limbs in (1, 2, 3), "conv: limbs")
     cout = codes.shape[0]
-    _req(codes.dtype == torch.int8 and codes.shape == (cout, kh * kw * cin) and codes.is_contiguous(), "conv: codes shape")
+    _req(codes.dtype == torch.int8 and codes.shape == (cout, kh * kw * cin) and codes.is_contiguous()
+         and codes.device == xq.device, "conv: codes shape")
     _req(cin % 64 == 0, "conv: cin must be a multiple of 64")
     _req(offset is None or (offset.dtype == torch.int32 and offset.numel() == cout), "conv: offset")
     _req(x_absmax.dtype == torch.float32 and x_absmax.numel() == n, "conv: x_absmax")
     for t in (col_scale, col_shift):
-        _req(t.dtype == torch.float32 and t.numel() == cout and t.is_contiguous() and t.device == x.device, "conv: col vectors")
+        _req(t.dtype == torch.float32 and t.numel() == cout and t.is_contiguous() and t.device == xq.device,
+             "conv: col vectors")
     ho = (h + 2 * pad - kh) // stride + 1
     wo = (w + 2 * pad - kw) // stride + 1
+    _req(ho > 0 and wo > 0, "conv: empty output")
     if out is None:
-        out = torch.empty(n, ho, wo, cout, dtype=torch.float32, device=x.device)
+        out = torch.empty(n, ho, wo, cout, dtype=torch.float32, device=xq.device)
     _req(out.shape == (n, ho, wo, cout) and out.is_contiguous(), "conv: out shape")
     if residual is not None:
         _req(residual.shape == (n, ho, wo, cout) and residual.is_contiguous() and residual.dtype == torch.float32,
@@ -125,14 +147,22 @@ def conv2d_nhwc(x, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_
     hook = _CONV_HOOK[0]
     if hook is not None:
         hook.begin()
-    with torch.cuda.device(x.device):
+    with torch.cuda.device(xq.device):
         _lib.check(lib.smpq_conv2d_fwd(
-            _lib.ptr(x), _lib.ptr(x_absmax), n, h, w, cin, _lib.ptr(codes), _lib.ptr(offset), cout, kh, kw,
+            _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, cin, _lib.ptr(codes), _lib.ptr(offset), cout, kh, kw,
             stride, pad, _lib.ptr(col_scale), _lib.ptr(col_shift), _lib.ptr(residual), 1 if relu else 0,
             int(limbs), _lib.ptr(out), _lib.ptr(y_absmax), _lib.stream_ptr()), "smpq_conv2d_fwd")
     if hook is not None:
         hook.end(2 * n * ho * wo * cout * kh * kw * cin, (n, h, w, cin, cout, kh, stride))
     return out
+
+
+def conv2d_nhwc(x, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
+                residual=None, relu=False, limbs=None, y_absmax=None, out=None):
+    """act_quantize + conv2d_q on an NHWC fp32 input."""
+    xq = act_quantize(x, x_absmax, limbs)
+    return conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
+                    residual=residual, relu=relu, y_absmax=y_absmax, out=out)
 
 
 def set_conv_hook(hook):

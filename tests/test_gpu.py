@@ -60,6 +60,25 @@ def test_device_quantizer_layer_matches_host(gpu):
     assert torch.equal(sd.cpu(), sh)
 
 
+@pytest.mark.parametrize("limbs", [1, 2, 3])
+def test_act_quantize_digits(gpu, limbs):
+    from smpq import ops
+    g = torch.Generator().manual_seed(limbs)
+    x = torch.randn(3, 5, 7, 64, generator=g) * torch.tensor([1.0, 30.0, 1e-3]).reshape(3, 1, 1, 1)
+    x[2] = 0.0  # an all-zero image (absmax 0) quantizes to 0
+    xd = x.to(gpu)
+    am = ops.act_absmax(xd)
+    q = ops.act_quantize(xd, am, limbs).cpu().numpy().astype(np.int64)
+    assert q.shape == (limbs, 3, 5, 7, 64) and q.min() >= -128 and q.max() <= 127
+    val = sum(q[l] * 256 ** l for l in range(limbs))
+    qmax = np.float32(LIMB_QMAX[limbs])
+    amn = am.cpu().numpy()
+    inv = np.where(amn > 0, qmax / np.where(amn > 0, amn, 1).astype(np.float32), 0).astype(np.float32)
+    exp = np.clip(np.rint((x.numpy() * inv[:, None, None, None]).astype(np.float32)), -qmax, qmax)
+    np.testing.assert_array_equal(val, exp.astype(np.int64))
+    assert np.abs(val[:2]).max() == int(qmax)
+
+
 # ----------------------------------------------------------------------------------------------
 def make_layer(gpu, cin, cout, k, seed, bits_choice=(8, 6, 4)):
     from smpq import ops
@@ -249,15 +268,30 @@ def test_model_logits_vs_reference(gpu, case, arch, assign, batch, limbs):
 
 
 def test_batch_invariance_and_determinism(gpu):
-    """Per-image activation ranges => each image's logits do not depend on the batch."""
+    """Per-image activation ranges => a quantized conv's output for an image does not depend on
+    the rest of the batch (bitwise). The whole model is deterministic per batch shape; across
+    batch shapes only the fp32 MIOpen stem/downsample/fc may pick other algorithms (tiny diffs)."""
+    from smpq import ops
+    wd, step, codes, offset = make_layer(gpu, 256, 256, 3, seed=21)
+    x = torch.relu(torch.randn(256, 14, 14, 256, generator=torch.Generator().manual_seed(4))).to(gpu)
+    shift = torch.zeros(256, device=gpu)
+
+    def run(xx):
+        return ops.conv2d_nhwc(xx, ops.act_absmax(xx), codes, offset, 3, 3, 1, 1, step, shift, relu=True)
+    y_big = run(x)
+    assert torch.equal(y_big, run(x))
+    assert torch.equal(y_big[100:103], run(x[100:103].contiguous()))
     net = build_model(gpu, "resnet18", "r18_u8")
-    x = torch.randn(256, 3, 224, 224, generator=torch.Generator().manual_seed(11)).to(gpu)
-    with torch.no_grad():
-        y_big = net(x)
-        y_big2 = net(x)
-        y_small = net(x[100:103].contiguous())
-    assert torch.equal(y_big, y_big2)
-    assert torch.equal(y_big[100:103], y_small)
+    xi = torch.randn(64, 3, 224, 224, generator=torch.Generator().manual_seed(11)).to(gpu)
+    prev = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True  # MIOpen fp32 stem/downsample algorithms
+    try:
+        with torch.no_grad():
+            a, b, c = net(xi), net(xi), net(xi[10:13].contiguous())
+    finally:
+        torch.backends.cudnn.deterministic = prev
+    assert torch.equal(a, b)
+    torch.testing.assert_close(a[10:13], c, rtol=1e-4, atol=1e-4)
 
 
 def test_dropin_gpu_quantizer_and_fp32_channels(gpu):
