@@ -145,6 +145,9 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if rank == 0:
+        print("autotuned tiles:", {"x".join(map(str, k[:8])): v for k, v in ops._TUNED.items()},
+              file=sys.stderr, flush=True)
     timer = ConvTimer()
     ops.set_conv_hook(timer)
     torch.cuda.synchronize()

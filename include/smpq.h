@@ -100,12 +100,17 @@ int smpq_act_quantize(const float* x, int n, int64_t per_image, const float* abs
  *   relu       0/1, applied last
  *   limbs      activation code width in int8 limbs: 1 (int8), 2 (int16), 3 (int24)
  *   y          device fp32 NHWC [n][ho][wo][cout]
- *   y_absmax   device fp32 [n] (caller-zeroed), receives max|y| per image, or NULL */
+ *   y_absmax   device fp32 [n] (caller-zeroed), receives max|y| per image, or NULL
+ *   tile_cfg   block tile configuration (smpq_conv2d_tile_config), or -1 for the built-in choice */
 int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                     const int8_t* codes, const int32_t* offset, int cout, int kh, int kw,
                     int stride, int pad, const float* col_scale, const float* col_shift,
                     const float* residual, int relu, int limbs, float* y, float* y_absmax,
-                    smpq_stream_t stream);
+                    int tile_cfg, smpq_stream_t stream);
+
+/* Tile configurations of smpq_conv2d_fwd (for autotuning): count, and BM x BN / threads. */
+int smpq_conv2d_num_tile_configs(void);
+int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads);
 
 /* Workspace the conv needs (none today; kept for ABI stability). */
 size_t smpq_conv2d_workspace_bytes(int n, int h, int w, int cin, int cout, int kh, int kw,

@@ -30,7 +30,6 @@
 
 namespace smpq {
 
-constexpr int kThreads = 256;
 constexpr int kKStep = 64;      // K per MFMA (i8 16x16x64)
 constexpr int kRowBytes = 80;   // LDS row stride for a 64-byte K slice (+16 B pad vs conflicts)
 
@@ -63,11 +62,15 @@ __device__ __forceinline__ void split_limbs(int q, int* d) {
   d[L - 1] = q;
 }
 
-template <int L, int WM, int WN>
-__global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
-  constexpr int BM = 32 * WM;
-  constexpr int BN = 32 * WN;
-  constexpr int BROWS = BN / 64;  // B rows loaded per thread per K step (4 threads per row)
+// Block = WAVES_M x WAVES_N waves; each wave owns WM x WN 16x16 subtiles.
+template <int L, int WAVES_M, int WAVES_N, int WM, int WN, int MINW>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(ConvArgs a) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int BM = 16 * WM * WAVES_M;
+  constexpr int BN = 16 * WN * WAVES_N;
+  constexpr int RPP = NT / 4;                  // 64-B rows covered per pass (4 threads per row)
+  constexpr int AR = (BM + RPP - 1) / RPP;     // A rows per thread per limb
+  constexpr int BROWS = (BN + RPP - 1) / RPP;  // B rows per thread
 
   // one LDS arena: K-loop operand buffers, then (after the loop) the fp32 output tile
   constexpr int kLoopBytes = 2 * L * BM * kRowBytes + 2 * BN * kRowBytes;
@@ -87,7 +90,7 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
 
   const int ntiles = (a.cout + BN - 1) / BN;
   const int m0 = (blockIdx.x / ntiles) * BM;
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
   const int hw_out = a.ho * a.wo;
 
   // ---- per-block row table: image index and activation step of each output row ----------
-  for (int r = tid; r < BM; r += kThreads) {
+  for (int r = tid; r < BM; r += NT) {
     const int m = m0 + r;
     int img = -1;
     float sc = 0.f;
@@ -109,15 +112,14 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
   }
 
   // ---- per-thread A load rows: input pixel base and top-left tap coordinate -----------------
-  constexpr int AR = BM / 64;   // A rows per thread per limb (4 threads x 16 B per 64-B row)
   const int piece = tid & 3;    // 16-B piece of a 64-B K slice
-  const int row0 = tid >> 2;    // rows row0 + 64*i (A) / row0 + 64*j (B)
+  const int row0 = tid >> 2;    // rows row0 + RPP*i (A) / row0 + RPP*j (B)
   int a_pix[AR];                // n*h*w pixel base, or -1 when the row is past M
   int a_ih[AR], a_iw[AR];
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
-    const int m = m0 + row0 + 64 * i;
-    if (m < a.M) {
+    const int m = m0 + row0 + RPP * i;
+    if (row0 + RPP * i < BM && m < a.M) {
       const int img = m / hw_out;
       const int rem = m - img * hw_out;
       const int oh = rem / a.wo;
@@ -154,9 +156,9 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < BROWS; ++j) {
-      const int col = n0 + row0 + 64 * j;
+      const int col = n0 + row0 + RPP * j;
       v4i v = {0, 0, 0, 0};
-      if (col < a.cout) {
+      if (row0 + RPP * j < BN && col < a.cout) {
         v = *reinterpret_cast<const v4i*>(a.codes + (size_t)col * a.K + ks * kKStep + 16 * piece);
       }
       rb[j] = v;
@@ -168,10 +170,10 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
     for (int l = 0; l < L; ++l)
 #pragma unroll
       for (int i = 0; i < AR; ++i)
-        *reinterpret_cast<v4i*>(&As[buf][l][row0 + 64 * i][16 * piece]) = ra[l][i];
+        if (row0 + RPP * i < BM) *reinterpret_cast<v4i*>(&As[buf][l][row0 + RPP * i][16 * piece]) = ra[l][i];
 #pragma unroll
     for (int j = 0; j < BROWS; ++j)
-      *reinterpret_cast<v4i*>(&Bs[buf][row0 + 64 * j][16 * piece]) = rb[j];
+      if (row0 + RPP * j < BN) *reinterpret_cast<v4i*>(&Bs[buf][row0 + RPP * j][16 * piece]) = rb[j];
   };
 
   v4i acc[L][WM][WN];
@@ -257,7 +259,7 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
   const bool vec_ok = (a.cout & 3) == 0;
   __syncthreads();
   if (a.residual) {
-    for (int e = tid; e < BM * V4; e += kThreads) {
+    for (int e = tid; e < BM * V4; e += NT) {
       const int r = e / V4, c4 = e - (e / V4) * V4;
       const int m = m0 + r, col = n0 + 4 * c4;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(kThreads, 2) void qconv_kernel(ConvArgs a) {
     }
   }
   __syncthreads();
-  for (int e = tid; e < BM * V4; e += kThreads) {
+  for (int e = tid; e < BM * V4; e += NT) {
     const int r = e / V4, c4 = e - (e / V4) * V4;
     const int m = m0 + r, col = n0 + 4 * c4;
     if (m >= a.M || col >= a.cout) continue;
@@ -420,15 +422,56 @@ __global__ void debug_mfma_kernel(const int8_t* a, const int8_t* b, int32_t* c) 
   for (int r = 0; r < 4; ++r) c[(4 * (lane >> 4) + r) * 16 + frow] = acc[r];
 }
 
-template <int L, int WM, int WN>
+template <int L, int WAVES_M, int WAVES_N, int WM, int WN, int MINW>
 static int launch(const ConvArgs& a, hipStream_t stream) {
-  constexpr int BM = 32 * WM, BN = 32 * WN;
+  if constexpr (L * WM * WN * 4 > 128) {
+    // more than 128 accumulator registers per lane: not instantiated (would spill)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: tile config too large for this limb count");
+  } else {
+  constexpr int BM = 16 * WM * WAVES_M, BN = 16 * WN * WAVES_N;
   const long mt = (a.M + BM - 1) / BM;
   const long nt = (a.cout + BN - 1) / BN;
   const long blocks = mt * nt;
   if (blocks > 0x7fffffffL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
-  hipLaunchKernelGGL((qconv_kernel<L, WM, WN>), dim3((unsigned)blocks), dim3(kThreads), 0, stream, a);
+  hipLaunchKernelGGL((qconv_kernel<L, WAVES_M, WAVES_N, WM, WN, MINW>), dim3((unsigned)blocks),
+                     dim3(64 * WAVES_M * WAVES_N), 0, stream, a);
   return check_hip(hipGetLastError(), "qconv_kernel launch");
+  }
+}
+
+// Tile configurations: {waves_m, waves_n, wm, wn} -> BM x BN block tile, 64*waves threads.
+struct TileCfg {
+  int wavesm, wavesn, wm, wn;
+};
+constexpr TileCfg kTileCfgs[] = {
+    {2, 2, 4, 4},  // 0: 128 x 128, 256 threads
+    {2, 2, 2, 4},  // 1:  64 x 128, 256 threads
+    {2, 2, 4, 2},  // 2: 128 x  64, 256 threads
+    {2, 2, 2, 2},  // 3:  64 x  64, 256 threads
+    {2, 4, 4, 2},  // 4: 128 x 128, 512 threads (waves 64 x 32)
+    {4, 2, 2, 4},  // 5: 128 x 128, 512 threads (waves 32 x 64)
+};
+constexpr int kNumTileCfgs = sizeof(kTileCfgs) / sizeof(kTileCfgs[0]);
+
+template <int L>
+static int launch_cfg(int cfg, const ConvArgs& a, hipStream_t s) {
+  switch (cfg) {
+    case 0: return launch<L, 2, 2, 4, 4, 2>(a, s);
+    case 1: return launch<L, 2, 2, 2, 4, 2>(a, s);
+    case 2: return launch<L, 2, 2, 4, 2, 2>(a, s);
+    case 3: return launch<L, 2, 2, 2, 2, 4>(a, s);
+    case 4: return launch<L, 2, 4, 4, 2, 4>(a, s);
+    case 5: return launch<L, 4, 2, 2, 4, 2>(a, s);
+    default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
+  }
+}
+
+// Default tile when the caller does not pass one (the Python layer autotunes per shape).
+static int heuristic_cfg(int L, long M, int cout, int K) {
+  if (cout <= 64) return M >= 128L * 512 ? 2 : 3;
+  if (L == 3) return K <= 256 ? 3 : 2;
+  if (K <= 256) return 1;
+  return 0;
 }
 
 }  // namespace smpq
@@ -439,7 +482,7 @@ extern "C" int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, i
                                const int8_t* codes, const int32_t* offset, int cout, int kh, int kw,
                                int stride, int pad, const float* col_scale, const float* col_shift,
                                const float* residual, int relu, int limbs, float* y, float* y_absmax,
-                               smpq_stream_t stream) {
+                               int tile_cfg, smpq_stream_t stream) {
   if (!xq || !x_absmax || !codes || !col_scale || !col_shift || !y)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: null pointer");
   if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || stride <= 0 ||
@@ -481,19 +524,33 @@ extern "C" int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, i
   a.relu = relu ? 1 : 0;
   a.has_offset = offset ? 1 : 0;
   hipStream_t s = (hipStream_t)stream;
+  if (tile_cfg < 0) tile_cfg = heuristic_cfg(limbs, M, cout, a.K);
+  if (tile_cfg >= kNumTileCfgs) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   switch (limbs) {
     case 1:
       a.inv_qmax = 1.f / 127.f;
-      return cout <= 64 ? launch<1, 4, 2>(a, s) : launch<1, 4, 4>(a, s);
+      return launch_cfg<1>(tile_cfg, a, s);
     case 2:
       a.inv_qmax = 1.f / 32512.f;
-      return cout <= 64 ? launch<2, 4, 2>(a, s) : launch<2, 4, 4>(a, s);
+      return launch_cfg<2>(tile_cfg, a, s);
     case 3:
       a.inv_qmax = 1.f / 8323072.f;
-      return launch<3, 4, 2>(a, s);
+      return launch_cfg<3>(tile_cfg, a, s);
     default:
       return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: limbs must be 1, 2 or 3");
   }
+}
+
+extern "C" int smpq_conv2d_num_tile_configs(void) { return kNumTileCfgs; }
+
+extern "C" int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads) {
+  if (cfg < 0 || cfg >= kNumTileCfgs || !bm || !bn || !threads)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_tile_config: bad arguments");
+  const TileCfg& t = kTileCfgs[cfg];
+  *bm = 16 * t.wm * t.wavesm;
+  *bn = 16 * t.wn * t.wavesn;
+  *threads = 64 * t.wavesm * t.wavesn;
+  return SMPQ_OK;
 }
 
 extern "C" int smpq_act_quantize(const float* x, int n, int64_t per_image, const float* absmax, int limbs,

@@ -41,7 +41,9 @@ _PROTOS = {
     "smpq_act_absmax": (_i, [_vp, _i, _i64, _vp, _vp]),
     "smpq_act_quantize": (_i, [_vp, _i, _i64, _vp, _i, _vp, _vp]),
     "smpq_conv2d_fwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp,
-                             _vp, _i, _i, _vp, _vp, _vp]),
+                             _vp, _i, _i, _vp, _vp, _i, _vp]),
+    "smpq_conv2d_num_tile_configs": (_i, []),
+    "smpq_conv2d_tile_config": (_i, [_i, _vp, _vp, _vp]),
     "smpq_conv2d_workspace_bytes": (ctypes.c_size_t, [_i] * 10),
     "smpq_debug_mfma_i8": (_i, [_vp, _vp, _vp, _vp]),
 }

@@ -3,6 +3,8 @@
 Every function validates shapes/dtypes/devices on the host before launching, so a kernel
 never sees an operand that disagrees with its grid (no device-side faults on bad input).
 """
+import os
+
 import torch
 
 from . import _lib
@@ -116,8 +118,24 @@ def act_quantize(x, x_absmax, limbs=None, out=None):
     return out
 
 
+_TILES = {}
+
+
+def tile_configs():
+    """{cfg: (BM, BN, threads)} of the conv kernel's block tiles."""
+    if not _TILES:
+        lib = _lib.load()
+        import ctypes
+        for c in range(lib.smpq_conv2d_num_tile_configs()):
+            bm, bn, nt = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+            _lib.check(lib.smpq_conv2d_tile_config(c, ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(nt)),
+                       "smpq_conv2d_tile_config")
+            _TILES[c] = (bm.value, bn.value, nt.value)
+    return _TILES
+
+
 def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
-             residual=None, relu=False, y_absmax=None, out=None):
+             residual=None, relu=False, y_absmax=None, out=None, tile_cfg=-1):
     """Quantized conv on int8 limb planes xq [L, n, h, w, cin] (from act_quantize):
     y = conv(x, codes) * s_x * col_scale + col_shift (+res) (relu), NHWC fp32."""
     _req(xq.is_cuda and xq.dtype == torch.int8 and xq.dim() == 5 and xq.is_contiguous(), "conv: xq must be [L,n,h,w,c] int8")
@@ -151,18 +169,61 @@ def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_sh
         _lib.check(lib.smpq_conv2d_fwd(
             _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, cin, _lib.ptr(codes), _lib.ptr(offset), cout, kh, kw,
             stride, pad, _lib.ptr(col_scale), _lib.ptr(col_shift), _lib.ptr(residual), 1 if relu else 0,
-            int(limbs), _lib.ptr(out), _lib.ptr(y_absmax), _lib.stream_ptr()), "smpq_conv2d_fwd")
+            int(limbs), _lib.ptr(out), _lib.ptr(y_absmax), int(tile_cfg), _lib.stream_ptr()), "smpq_conv2d_fwd")
     if hook is not None:
         hook.end(2 * n * ho * wo * cout * kh * kw * cin, (n, h, w, cin, cout, kh, stride))
     return out
 
 
+# ---- per-shape autotuning of the block tile (cf. cudnn.benchmark=True, resnet50_main.py:10) ----
+AUTOTUNE = [os.environ.get("SMPQ_AUTOTUNE", "1") != "0"]
+_TUNED = {}
+
+
+def _tile_fits(cfg, limbs):
+    bm, bn, nt = tile_configs()[cfg]
+    waves = nt // 64
+    return limbs * (bm // 16) * (bn // 16) // waves * 4 <= 128
+
+
+def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
+                   residual=None, relu=False, y_absmax=None, out=None):
+    """conv2d_q with the fastest tile for this shape (timed once per shape, then cached).
+    Every tile gives bitwise-identical results (exact integer accumulation, same epilogue)."""
+    limbs, n, h, w, cin = xq.shape
+    key = (n, h, w, cin, codes.shape[0], kh, kw, stride, pad, limbs, residual is not None)
+    cfg = _TUNED.get(key)
+    if cfg is None and AUTOTUNE[0] and not torch.cuda.is_current_stream_capturing():
+        best = None
+        for c in tile_configs():
+            if not _tile_fits(c, limbs):
+                continue
+            times = []
+            for rep in range(3):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                out = conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
+                               residual=residual, relu=relu, y_absmax=y_absmax, out=out, tile_cfg=c)
+                e1.record()
+                times.append((e0, e1))
+            torch.cuda.synchronize()
+            t = min(a.elapsed_time(b) for a, b in times[1:])
+            if best is None or t < best[0]:
+                best = (t, c)
+        cfg = best[1]
+        _TUNED[key] = cfg
+    return conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
+                    residual=residual, relu=relu, y_absmax=y_absmax, out=out,
+                    tile_cfg=-1 if cfg is None else cfg)
+
+
 def conv2d_nhwc(x, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
                 residual=None, relu=False, limbs=None, y_absmax=None, out=None):
-    """act_quantize + conv2d_q on an NHWC fp32 input."""
+    """act_quantize + (autotuned) conv2d_q on an NHWC fp32 input."""
     xq = act_quantize(x, x_absmax, limbs)
-    return conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
-                    residual=residual, relu=relu, y_absmax=y_absmax, out=out)
+    return tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
+                          residual=residual, relu=relu, y_absmax=y_absmax, out=out)
 
 
 def set_conv_hook(hook):

@@ -209,6 +209,33 @@ def test_conv_limbs_and_edges(gpu, shape, limbs):
     run_conv_case(gpu, cin, cout, k, s, h, limbs=limbs, seed=7 * cin + cout, signed=True, residual=True, relu=True, batch=3)
 
 
+@pytest.mark.parametrize("limbs", [1, 2, 3])
+@pytest.mark.parametrize("shape", [(64, 256, 1, 1, 20), (128, 128, 3, 2, 17), (64, 80, 3, 1, 9), (256, 48, 1, 1, 7)],
+                         ids=lambda s: "c%d_o%d_k%d_s%d_h%d" % s)
+def test_all_tile_configs_bitwise_identical(gpu, shape, limbs):
+    from smpq import ops
+    cin, cout, k, s, h = shape
+    wd, step, codes, offset = make_layer(gpu, cin, cout, k, seed=cin + 3 * cout)
+    x = torch.randn(3, h, h, cin, generator=torch.Generator().manual_seed(9)).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, limbs)
+    ho = (h + 2 * (k // 2) - k) // s + 1
+    res = torch.randn(3, ho, ho, cout, generator=torch.Generator().manual_seed(10)).to(gpu)
+    shift = torch.linspace(-1, 1, cout, device=gpu)
+    outs = []
+    for c in ops.tile_configs():
+        if not ops._tile_fits(c, limbs):
+            continue
+        ya = torch.zeros(3, device=gpu)
+        y = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, residual=res, relu=True,
+                         y_absmax=ya, tile_cfg=c)
+        outs.append((c, y, ya))
+    assert len(outs) >= 3
+    for c, y, ya in outs[1:]:
+        assert torch.equal(y, outs[0][1]), c
+        assert torch.equal(ya, outs[0][2]), c
+
+
 def test_conv_offsets_exercised(gpu):
     # 8-bit channels need a code offset whenever their code range is not inside [-128, 127]
     off = run_conv_case(gpu, 256, 256, 1, 1, 14, limbs=2, seed=3)
