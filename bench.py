@@ -123,7 +123,7 @@ def main():
         dist.barrier()
         __graft_entry__.build()
     import resnet
-    from smpq import assignments, ops, stats
+    from smpq import assignments, dp, ops, stats
 
     arch, assign, desc = CONFIGS[args.config]
     ops.set_act_limbs(args.limbs)
@@ -131,17 +131,16 @@ def main():
     net = getattr(resnet, arch)().to(dev).eval()
     assignments.apply_assignment(net, assign)
 
-    # synthetic input shard of the global batch, generated on device (rank r: images r*B..)
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    x = torch.randn(args.batch, 3, 224, 224, generator=g, device=dev)
+    # this rank's shard of the global batch (dp.shard_range), generated on device
+    s0, s1 = dp.shard_range(args.batch * world, rank, world)
+    g = torch.Generator(device=dev).manual_seed(1000 + s0)
+    x = torch.randn(s1 - s0, 3, 224, 224, generator=g, device=dev)
     gathered = torch.empty(world * args.batch, 1000, device=dev) if world > 1 else None
 
     def step():
         with torch.no_grad():
             y = net(x)
-            if world > 1:
-                dist.all_gather_into_tensor(gathered, y.contiguous())
-        return y
+            return dp.gather_logits(y, world, out=gathered)
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,69 @@
+"""World-size-2 gloo tests of the data-parallel sharding + logits all-gather (CPU)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model(x):
+    # a per-image deterministic function standing in for the network
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(x[0].numel(), 10, generator=g)
+    return x.flatten(1) @ w
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "semilayer-wise-mixed-precision-quantization_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from smpq import dp
+        x = torch.randn(8, 3, 4, 4, generator=torch.Generator().manual_seed(1))
+        y = dp.sharded_forward(_model, x, rank, world)
+        q.put((rank, y))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_forward_equals_single_process(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    x = torch.randn(8, 3, 4, 4, generator=torch.Generator().manual_seed(1))
+    ref = _model(x)
+    for r in range(world):
+        assert torch.equal(res[r], ref)
+
+
+def test_shard_range_covers_batch():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "semilayer-wise-mixed-precision-quantization_amd"))
+    from smpq import dp
+    for b in (1, 7, 256, 2048):
+        for w in (1, 2, 3, 8):
+            spans = [dp.shard_range(b, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == b
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
