@@ -77,6 +77,22 @@ int smpq_quantize_channels_host(float* w, int cout, int k_elems, const int8_t* b
 int smpq_pack_weights(const float* w, int cout, int cin, int kh, int kw, const float* step,
                       int8_t* codes, int32_t* offset, int32_t* status, smpq_stream_t stream);
 
+/* General weight packer for smpq_conv2d_fwd_ex: `wlimbs` int8 planes codes[wlimbs][cout][K].
+ *   step     device fp32 [cout] recorded quantization step, 0 = never quantized (may be NULL
+ *            when wlimbs == 2: every channel then uses 16-bit fixed point)
+ *   wlimbs   1: exact int8 codes (m - offset) of quantized channels (status[0]/[1] report
+ *            channels that cannot be coded); 2 / 3: exact codes of quantized channels that fit
+ *            16 / 24 bits, per-channel fixed point (max|w| / 32512 or / 8323072) for the others
+ *            (status[2] counts them)
+ *   cin      <= 4 (stem: channels padded to 4, K = ceil(kh*kw/16)*64) or a multiple of 64
+ *            (K = kh*kw*cin, ordered [kh][kw][cin])
+ *   offset   device int32 [cout] (wlimbs == 1), wscale device fp32 [cout]: the per-channel weight
+ *            step the codes are in (= step for exact channels)
+ *   status   device int32 [3], caller-zeroed */
+int smpq_pack_weights_ex(const float* w, int cout, int cin, int kh, int kw, const float* step,
+                         int wlimbs, int8_t* codes, int32_t* offset, float* wscale, int32_t* status,
+                         smpq_stream_t stream);
+
 /* Per-image absolute maximum, accumulated with atomicMax into absmax[n] (caller zeroes). */
 int smpq_act_absmax(const float* x, int n, int64_t per_image, float* absmax,
                     smpq_stream_t stream);
@@ -89,6 +105,18 @@ int smpq_act_absmax(const float* x, int n, int64_t per_image, float* absmax,
  *   out      device int8 [limbs][n * per_image] */
 int smpq_act_quantize(const float* x, int n, int64_t per_image, const float* absmax, int limbs,
                       int8_t* out, smpq_stream_t stream);
+
+/* Image batch NCHW fp32 [n][c][h][w] (c <= 4) -> `limbs` int8 planes NHWC with 4 channels
+ * (zero padded): the stem conv's input (resnet.py:143). absmax from smpq_act_absmax. */
+int smpq_image_quantize(const float* x, int n, int c, int h, int w, const float* absmax, int limbs,
+                        int8_t* out, smpq_stream_t stream);
+
+/* MaxPool2d(3, stride 2, pad 1) (resnet.py:147) on NHWC fp32 [n][h][w][c] (c % 4 == 0), fused
+ * with the activation quantizer of its output: `limbs` int8 planes [n][ho][wo][c] with the
+ * per-image range absmax (the pool input's max; equal to the output's for ReLU outputs).
+ * out_f32: optional fp32 NHWC pooled output (NULL to skip). */
+int smpq_maxpool_quantize(const float* x, int n, int h, int w, int c, const float* absmax, int limbs,
+                          int8_t* out, float* out_f32, smpq_stream_t stream);
 
 /* Quantized conv forward (implicit GEMM on int8 MFMA), NHWC.
  *   xq         device int8 [limbs][n][h][w][cin] digit planes from smpq_act_quantize; cin % 64 == 0
@@ -107,6 +135,29 @@ int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w
                     int stride, int pad, const float* col_scale, const float* col_shift,
                     const float* residual, int relu, int limbs, float* y, float* y_absmax,
                     int tile_cfg, smpq_stream_t stream);
+
+/* smpq_conv2d_fwd with weight limbs (1, 2, or 3 with limbs == 3): codes [wlimbs][cout][K] from
+ * smpq_pack_weights_ex, and
+ * cin == 4 (stem, K padded) supported besides cin % 64 == 0. col_scale must include the
+ * per-channel weight step (wscale) of the packer. */
+int smpq_conv2d_fwd_ex(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+                       const int8_t* codes, int wlimbs, const int32_t* offset, int cout, int kh,
+                       int kw, int stride, int pad, const float* col_scale, const float* col_shift,
+                       const float* residual, int relu, int limbs, float* y, float* y_absmax,
+                       int tile_cfg, smpq_stream_t stream);
+
+/* smpq_conv2d_fwd_ex that can also (or only) emit the NEXT conv's activation limb planes:
+ *   y          fp32 NHWC output, or NULL when only yq is wanted
+ *   yq         int8 [limbs][n*ho*wo][cout] planes of q = clamp(rne(y * QMAX / yq_range)), or NULL
+ *   yq_range   static per-layer range (> 0) of the output quantizer (calibrated by the caller)
+ *   overflow   device int32 [1]: set to 1 when some |y| > yq_range (values are then clamped; the
+ *              caller re-runs with dynamic ranges) */
+int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+                      const int8_t* codes, int wlimbs, const int32_t* offset, int cout, int kh,
+                      int kw, int stride, int pad, const float* col_scale, const float* col_shift,
+                      const float* residual, int relu, int limbs, float* y, float* y_absmax,
+                      int8_t* yq, float yq_range, int32_t* overflow, int tile_cfg,
+                      smpq_stream_t stream);
 
 /* Tile configurations of smpq_conv2d_fwd (for autotuning): count, and BM x BN / threads. */
 int smpq_conv2d_num_tile_configs(void);

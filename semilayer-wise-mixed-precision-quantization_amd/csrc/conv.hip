@@ -1,49 +1,56 @@
 // Quantized convolution forward for gfx950 (CDNA4): implicit GEMM on int8 MFMA.
 //
 // Replaces nn.Conv2d on the fake-quantized weight (resnet.py:22-30) together with the eval
-// BatchNorm, ReLU and residual add that follow it (resnet.py:55-68 / 97-116).
+// BatchNorm, ReLU and residual add that follow it (resnet.py:55-68 / 97-116), and the
+// unquantized stem / downsample convs (resnet.py:143, 188-192).
 //
-// GEMM view (NHWC activations, K ordered [kh][kw][cin]):
-//   M = n*ho*wo output pixels, N = cout, K = kh*kw*cin (cin % 64 == 0: one 64-wide K step is
-//   64 contiguous input channels of a single tap, i.e. one 256-B fp32 run of one NHWC pixel).
-//   A[m][k] = activation code of x at the tap's input pixel (0 outside the image: zero pad)
-//   B[k][n] = weight code m_n,k - offset_n (int8, from smpq_pack_weights)
+// GEMM view (NHWC activations):
+//   M = n*ho*wo output pixels, N = cout, K = kh*kw*cin ordered [kh][kw][cin].
+//   * cin % 64 == 0: one 64-wide K step is 64 contiguous channels of one tap (64 B per limb).
+//   * cin == 4 (the stem: RGB padded to 4): one K step is 16 taps x 4 channels; K is padded
+//     with zero weights to a multiple of 64.
+//   A[m][k] = activation code at the tap's input pixel (0 outside the image: zero padding).
+//   B[k][n] = weight code (int8 limbs, from smpq_pack_weights_ex).
 //
-// Exactness of the weight side: the reference weight is w = fl32(m * step) (functions.py:41);
-// the kernel multiplies the integer code m (exact) and applies `step` once per output, so the
-// only weight-side difference is the <= 2^-24 relative rounding inside fl32(m * step).
+// Weights: LW int8 limbs. LW = 1: the reference's integer codes m (functions.py:41: the weight is
+// exactly fl32(m * step)), centred by a per-channel offset when needed — exact. LW = 2 / 3: 16 /
+// 24-bit per-channel fixed point for fp32 (unquantized) weights (LW follows the activation width),
+// or exact codes that do not fit int8.
+// Activations: L int8 limbs of a per-image fixed point q = rne(x * QMAX / max|x_img|)
+// (act_quantize_kernel), L = 1 / 2 / 3 -> int8 / int16 / int24.
+// Each (activation limb, weight limb) pair is one MFMA pass; passes of equal total weight
+// 256^(la+lw) share an int32 accumulator; the NACC = L + LW - 1 accumulators are recombined in
+// fp32 in the epilogue. All accumulation is exact integer arithmetic, so results are independent
+// of the tile configuration and of the batch composition (per-image steps).
 //
-// Activation side: x is quantized ONCE per element by act_quantize_kernel with a per-image step
-// s_x = max|x_img| / QMAX into an integer q with `L` balanced base-256 int8 digits (limbs),
-// q = sum_l 256^l d_l, stored as L int8 planes (NHWC each). L = 1 gives int8, L = 2 int16,
-// L = 3 int24 fixed point. The GEMM copies limb bytes straight into LDS; each limb is one MFMA
-// pass over the same B fragment, accumulated in its own int32 accumulator and recombined in
-// fp32 in the epilogue. Per-image steps make every image's result independent of the batch.
-//
-// Tile: 256 threads = 4 waves as 2 (M) x 2 (N); each wave owns WM x WN subtiles of 16 x 16
-// computed with v_mfma_i32_16x16x64_i8 (one K step of 64 per MFMA). Block tile
-// BM = 32*WM rows x BN = 32*WN columns. Global -> register prefetch of step k+1 overlaps the
-// MFMAs of step k; one LDS double buffer, one barrier per K step.
+// Tile: WAVES_M x WAVES_N waves; each wave owns WM x WN subtiles of 16 x 16 computed with
+// v_mfma_i32_16x16x64_i8. Global -> register prefetch of K step k+1 overlaps the MFMAs of step
+// k; one LDS double buffer, one barrier per K step; the epilogue reuses the LDS arena as an fp32
+// output tile so residual loads and output stores are whole 16-B pieces of contiguous rows.
 #include <string>
 
 #include "common.h"
 
 namespace smpq {
 
-constexpr int kKStep = 64;      // K per MFMA (i8 16x16x64)
-constexpr int kRowBytes = 80;   // LDS row stride for a 64-byte K slice (+16 B pad vs conflicts)
+constexpr int kKStep = 64;     // K per MFMA (i8 16x16x64)
+constexpr int kRowBytes = 80;  // LDS row stride for a 64-byte K slice (+16 B pad vs conflicts)
 
 struct ConvArgs {
-  const int8_t* xq;
-  long long plane;
-  const float* x_absmax;
-  const int8_t* codes;
-  const int32_t* w_off;
+  const int8_t* xq;      // [L][n][h][w][cin] activation limb planes
+  long long plane;       // elements per activation plane
+  const float* x_absmax; // [n]
+  const int8_t* codes;   // [LW][cout][K] weight limb planes
+  long long wplane;      // elements per weight plane (cout*K)
+  const int32_t* w_off;  // [cout] (LW == 1 only) or NULL
   const float* col_scale;
   const float* col_shift;
   const float* residual;
-  float* y;
+  float* y;              // fp32 NHWC output, or NULL
   float* y_absmax;
+  int8_t* yq;            // [L][M][cout] output limb planes (static range), or NULL
+  float yq_inv;          // QMAX / range of the output quantizer
+  int32_t* overflow;     // set to 1 when |y| exceeded the static range (then clamped)
   int n, h, w, cin, cout, kh, kw, stride, pad, ho, wo;
   int M, K, ksteps, cchunks;
   int relu, has_offset;
@@ -62,26 +69,33 @@ __device__ __forceinline__ void split_limbs(int q, int* d) {
   d[L - 1] = q;
 }
 
+template <int L>
+__device__ __host__ constexpr float act_qmax() {
+  return L == 1 ? 127.f : (L == 2 ? 32512.f : 8323072.f);
+}
+
 // Block = WAVES_M x WAVES_N waves; each wave owns WM x WN 16x16 subtiles.
-template <int L, int WAVES_M, int WAVES_N, int WM, int WN, int MINW>
+template <int L, int LW, bool SMALLC, int WAVES_M, int WAVES_N, int WM, int WN, int MINW>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(ConvArgs a) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int BM = 16 * WM * WAVES_M;
   constexpr int BN = 16 * WN * WAVES_N;
+  constexpr int NACC = L + LW - 1;
   constexpr int RPP = NT / 4;                  // 64-B rows covered per pass (4 threads per row)
   constexpr int AR = (BM + RPP - 1) / RPP;     // A rows per thread per limb
-  constexpr int BROWS = (BN + RPP - 1) / RPP;  // B rows per thread
+  constexpr int BROWS = (BN + RPP - 1) / RPP;  // B rows per thread per limb
 
   // one LDS arena: K-loop operand buffers, then (after the loop) the fp32 output tile
-  constexpr int kLoopBytes = 2 * L * BM * kRowBytes + 2 * BN * kRowBytes;
+  constexpr int kABytes = 2 * L * BM * kRowBytes;
+  constexpr int kLoopBytes = kABytes + 2 * LW * BN * kRowBytes;
   constexpr int TS = BN + 4;  // epilogue tile row stride (floats): conflict-free lane writes
   constexpr int kEpiBytes = BM * TS * 4;
   constexpr int kArena = kLoopBytes > kEpiBytes ? kLoopBytes : kEpiBytes;
   __shared__ __attribute__((aligned(16))) int8_t arena[kArena];
   typedef int8_t ATile[L][BM][kRowBytes];
-  typedef int8_t BTile[BN][kRowBytes];
+  typedef int8_t BTile[LW][BN][kRowBytes];
   ATile* As = reinterpret_cast<ATile*>(arena);
-  BTile* Bs = reinterpret_cast<BTile*>(arena + 2 * L * BM * kRowBytes);
+  BTile* Bs = reinterpret_cast<BTile*>(arena + kABytes);
   float* tile = reinterpret_cast<float*>(arena);
   __shared__ float s_rowscale[BM];
   __shared__ int s_rowimg[BM];
@@ -112,9 +126,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
   }
 
   // ---- per-thread A load rows: input pixel base and top-left tap coordinate -----------------
-  const int piece = tid & 3;    // 16-B piece of a 64-B K slice
-  const int row0 = tid >> 2;    // rows row0 + RPP*i (A) / row0 + RPP*j (B)
-  int a_pix[AR];                // n*h*w pixel base, or -1 when the row is past M
+  const int piece = tid & 3;  // 16-B piece of a 64-B K slice
+  const int row0 = tid >> 2;  // rows row0 + RPP*i (A) / row0 + RPP*j (B)
+  int a_pix[AR];              // n*h*w pixel base, or -1 when the row is past M
   int a_ih[AR], a_iw[AR];
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
@@ -134,34 +148,60 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
   }
 
   v4i ra[L][AR];
-  v4i rb[BROWS];
+  v4i rb[LW][BROWS];
 
   auto load_global = [&](int ks) {
-    const int tap = ks / a.cchunks;
-    const int c0 = (ks - tap * a.cchunks) * kKStep;
-    const int kr = tap / a.kw;
-    const int kc = tap - kr * a.kw;
+    if constexpr (SMALLC) {
+      // 16 taps x 4 channels per K step; this thread's piece = taps 16*ks + 4*piece + 0..3
+      const int taps = a.kh * a.kw;
 #pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int ih = a_ih[i] + kr;
-      const int iw = a_iw[i] + kc;
-      const bool ok = a_pix[i] >= 0 && (unsigned)ih < (unsigned)a.h && (unsigned)iw < (unsigned)a.w;
-      const size_t off = ok ? ((size_t)(a_pix[i] + ih * a.w + iw) * a.cin + c0 + 16 * piece) : 0;
+      for (int i = 0; i < AR; ++i) {
+        int v[L][4];
 #pragma unroll
-      for (int l = 0; l < L; ++l) {
-        v4i v = {0, 0, 0, 0};
-        if (ok) v = *reinterpret_cast<const v4i*>(a.xq + l * a.plane + off);
-        ra[l][i] = v;
+        for (int t = 0; t < 4; ++t) {
+          const int tap = 16 * ks + 4 * piece + t;
+          const int kr = tap / a.kw, kc = tap - (tap / a.kw) * a.kw;
+          const int ih = a_ih[i] + kr, iw = a_iw[i] + kc;
+          const bool ok = tap < taps && a_pix[i] >= 0 && (unsigned)ih < (unsigned)a.h &&
+                          (unsigned)iw < (unsigned)a.w;
+          const size_t off = ok ? (size_t)(a_pix[i] + ih * a.w + iw) * 4 : 0;
+#pragma unroll
+          for (int l = 0; l < L; ++l)
+            v[l][t] = ok ? *reinterpret_cast<const int*>(a.xq + l * a.plane + off) : 0;
+        }
+#pragma unroll
+        for (int l = 0; l < L; ++l) ra[l][i] = v4i{v[l][0], v[l][1], v[l][2], v[l][3]};
+      }
+    } else {
+      const int tap = ks / a.cchunks;
+      const int c0 = (ks - tap * a.cchunks) * kKStep;
+      const int kr = tap / a.kw;
+      const int kc = tap - kr * a.kw;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const int ih = a_ih[i] + kr;
+        const int iw = a_iw[i] + kc;
+        const bool ok = a_pix[i] >= 0 && (unsigned)ih < (unsigned)a.h && (unsigned)iw < (unsigned)a.w;
+        const size_t off = ok ? ((size_t)(a_pix[i] + ih * a.w + iw) * a.cin + c0 + 16 * piece) : 0;
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+          v4i v = {0, 0, 0, 0};
+          if (ok) v = *reinterpret_cast<const v4i*>(a.xq + l * a.plane + off);
+          ra[l][i] = v;
+        }
       }
     }
 #pragma unroll
     for (int j = 0; j < BROWS; ++j) {
       const int col = n0 + row0 + RPP * j;
-      v4i v = {0, 0, 0, 0};
-      if (row0 + RPP * j < BN && col < a.cout) {
-        v = *reinterpret_cast<const v4i*>(a.codes + (size_t)col * a.K + ks * kKStep + 16 * piece);
+      const bool ok = row0 + RPP * j < BN && col < a.cout;
+      const size_t off = ok ? (size_t)col * a.K + ks * kKStep + 16 * piece : 0;
+#pragma unroll
+      for (int lw = 0; lw < LW; ++lw) {
+        v4i v = {0, 0, 0, 0};
+        if (ok) v = *reinterpret_cast<const v4i*>(a.codes + lw * a.wplane + off);
+        rb[lw][j] = v;
       }
-      rb[j] = v;
     }
   };
 
@@ -172,44 +212,51 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
       for (int i = 0; i < AR; ++i)
         if (row0 + RPP * i < BM) *reinterpret_cast<v4i*>(&As[buf][l][row0 + RPP * i][16 * piece]) = ra[l][i];
 #pragma unroll
-    for (int j = 0; j < BROWS; ++j)
-      if (row0 + RPP * j < BN) *reinterpret_cast<v4i*>(&Bs[buf][row0 + RPP * j][16 * piece]) = rb[j];
+    for (int lw = 0; lw < LW; ++lw)
+#pragma unroll
+      for (int j = 0; j < BROWS; ++j)
+        if (row0 + RPP * j < BN) *reinterpret_cast<v4i*>(&Bs[buf][lw][row0 + RPP * j][16 * piece]) = rb[lw][j];
   };
 
-  v4i acc[L][WM][WN];
-  int rs[L][WM];  // per-lane partial row sums of A codes (only for offset correction)
+  v4i acc[NACC][WM][WN];
+  int rs[L][WM];  // per-lane partial row sums of A codes (LW == 1 offset correction)
+#pragma unroll
+  for (int s = 0; s < NACC; ++s)
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j) acc[s][i][j] = v4i{0, 0, 0, 0};
 #pragma unroll
   for (int l = 0; l < L; ++l)
 #pragma unroll
-    for (int i = 0; i < WM; ++i) {
-      rs[l][i] = 0;
-#pragma unroll
-      for (int j = 0; j < WN; ++j) acc[l][i][j] = v4i{0, 0, 0, 0};
-    }
+    for (int i = 0; i < WM; ++i) rs[l][i] = 0;
 
   load_global(0);
   store_lds(0);
   __syncthreads();
 
-  const int frow = lane & 15;         // fragment row/col owned by this lane
-  const int fk = 16 * (lane >> 4);    // fragment K byte offset owned by this lane
+  const int frow = lane & 15;       // fragment row/col owned by this lane
+  const int fk = 16 * (lane >> 4);  // fragment K byte offset owned by this lane
   const int arow_base = wm * 16 * WM;
   const int bcol_base = wn * 16 * WN;
+  const bool do_off = (LW == 1) && a.has_offset;
 
   for (int ks = 0; ks < a.ksteps; ++ks) {
     const int buf = ks & 1;
     if (ks + 1 < a.ksteps) load_global(ks + 1);
 
-    v4i bf[WN];
+    v4i bf[LW][WN];
 #pragma unroll
-    for (int j = 0; j < WN; ++j)
-      bf[j] = *reinterpret_cast<const v4i*>(&Bs[buf][bcol_base + 16 * j + frow][fk]);
+    for (int lw = 0; lw < LW; ++lw)
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        bf[lw][j] = *reinterpret_cast<const v4i*>(&Bs[buf][lw][bcol_base + 16 * j + frow][fk]);
 #pragma unroll
     for (int l = 0; l < L; ++l) {
 #pragma unroll
       for (int i = 0; i < WM; ++i) {
         const v4i af = *reinterpret_cast<const v4i*>(&As[buf][l][arow_base + 16 * i + frow][fk]);
-        if (a.has_offset) {
+        if (do_off) {
           int s = rs[l][i];
           s = __builtin_amdgcn_sdot4(af.x, 0x01010101, s, false);
           s = __builtin_amdgcn_sdot4(af.y, 0x01010101, s, false);
@@ -218,8 +265,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
           rs[l][i] = s;
         }
 #pragma unroll
-        for (int j = 0; j < WN; ++j)
-          acc[l][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[j], acc[l][i][j], 0, 0, 0);
+        for (int lw = 0; lw < LW; ++lw)
+#pragma unroll
+          for (int j = 0; j < WN; ++j)
+            acc[l + lw][i][j] =
+                __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[lw][j], acc[l + lw][i][j], 0, 0, 0);
       }
     }
 
@@ -229,7 +279,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
 
   // ---- epilogue: recombine limbs, affine (dequant * BN), residual, ReLU, store, absmax ----
   // row sums: lanes {l, l^16, l^32, l^48} hold the four K quarters of row (l & 15)
-  if (a.has_offset) {
+  if (do_off) {
 #pragma unroll
     for (int l = 0; l < L; ++l)
 #pragma unroll
@@ -249,7 +299,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
     const bool ok = col < a.cout;
     colscale[j] = ok ? a.col_scale[col] : 0.f;
     colshift[j] = ok ? a.col_shift[col] : 0.f;
-    coloff[j] = (ok && a.has_offset) ? a.w_off[col] : 0;
+    coloff[j] = (ok && do_off) ? a.w_off[col] : 0;
   }
 
   // The K-loop buffers are dead: the arena becomes the [BM][TS] fp32 output tile. All global
@@ -287,8 +337,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
       const float rscale = s_rowscale[rloc];
       int rsum[L];
 #pragma unroll
-      for (int l = 0; l < L; ++l)
-        rsum[l] = a.has_offset ? __shfl(rs[l][i], 4 * (lane >> 4) + r, kWave) : 0;
+      for (int l = 0; l < L; ++l) rsum[l] = do_off ? __shfl(rs[l][i], 4 * (lane >> 4) + r, kWave) : 0;
       float rmax = 0.f;
 #pragma unroll
       for (int j = 0; j < WN; ++j) {
@@ -296,8 +345,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
         float v = 0.f;
         float limbw = 1.f;
 #pragma unroll
-        for (int l = 0; l < L; ++l) {
-          const int t = acc[l][i][j][r] + coloff[j] * rsum[l];
+        for (int s = 0; s < NACC; ++s) {
+          int t = acc[s][i][j][r];
+          if (s < L) t += coloff[j] * rsum[s];
           v += (float)t * limbw;
           limbw *= 256.f;
         }
@@ -319,26 +369,58 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
     }
   }
   __syncthreads();
+  bool ovf = false;
   for (int e = tid; e < BM * V4; e += NT) {
     const int r = e / V4, c4 = e - (e / V4) * V4;
     const int m = m0 + r, col = n0 + 4 * c4;
     if (m >= a.M || col >= a.cout) continue;
     const float4 v = *reinterpret_cast<const float4*>(&tile[r * TS + 4 * c4]);
-    float* dst = a.y + (size_t)m * a.cout + col;
-    if (vec_ok && col + 3 < a.cout) {
-      *reinterpret_cast<float4*>(dst) = v;
-    } else {
-      dst[0] = v.x;
-      if (col + 1 < a.cout) dst[1] = v.y;
-      if (col + 2 < a.cout) dst[2] = v.z;
-      if (col + 3 < a.cout) dst[3] = v.w;
+    if (a.y) {
+      float* dst = a.y + (size_t)m * a.cout + col;
+      if (vec_ok && col + 3 < a.cout) {
+        *reinterpret_cast<float4*>(dst) = v;
+      } else {
+        dst[0] = v.x;
+        if (col + 1 < a.cout) dst[1] = v.y;
+        if (col + 2 < a.cout) dst[2] = v.z;
+        if (col + 3 < a.cout) dst[3] = v.w;
+      }
+    }
+    if (a.yq) {
+      // fused activation quantizer of the NEXT conv's input (static per-layer range)
+      constexpr float qmax = act_qmax<L>();
+      const float vals[4] = {v.x, v.y, v.z, v.w};
+      unsigned int word[L];
+#pragma unroll
+      for (int l = 0; l < L; ++l) word[l] = 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float qf = rintf(vals[k] * a.yq_inv);
+        ovf |= fabsf(qf) > qmax;
+        qf = fminf(fmaxf(qf, -qmax), qmax);
+        int d[L];
+        split_limbs<L>((int)qf, d);
+#pragma unroll
+        for (int l = 0; l < L; ++l) word[l] |= (unsigned int)(d[l] & 255) << (8 * k);
+      }
+      int8_t* dq = a.yq + (size_t)m * a.cout + col;
+      const long long yplane = (long long)a.M * a.cout;
+      if (vec_ok && col + 3 < a.cout) {
+#pragma unroll
+        for (int l = 0; l < L; ++l) *reinterpret_cast<unsigned int*>(dq + l * yplane) = word[l];
+      } else {
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+          for (int k = 0; k < 4 && col + k < a.cout; ++k) dq[l * yplane + k] = (int8_t)(word[l] >> (8 * k));
+      }
     }
   }
+  if (a.yq && __any(ovf) && lane == 0) atomicMax(a.overflow, 1);
 
   if (a.y_absmax) {
     if (wave == 0) {
       const int img_lo = s_rowimg[0];
-      int last = min(BM, a.M - m0) - 1;
+      const int last = min(BM, a.M - m0) - 1;
       const int img_hi = s_rowimg[last];
       for (int img = img_lo; img <= img_hi; ++img) {
         float v = 0.f;
@@ -358,8 +440,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
 template <int L>
 __global__ __launch_bounds__(256) void act_quantize_kernel(const float* __restrict__ x, long long total,
                                                            long long per_image,
-                                                           const float* __restrict__ absmax, float qmax,
+                                                           const float* __restrict__ absmax,
                                                            int8_t* __restrict__ out, long long plane) {
+  const float qmax = act_qmax<L>();
   const long long nvec = total / 8;
   for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec;
        v += (long long)gridDim.x * blockDim.x) {
@@ -392,6 +475,93 @@ __global__ __launch_bounds__(256) void act_quantize_kernel(const float* __restri
   }
 }
 
+// NCHW fp32 image batch (c <= 4 channels) -> L int8 limb planes, NHWC with 4 channels (zero pad).
+template <int L>
+__global__ __launch_bounds__(256) void image_quantize_kernel(const float* __restrict__ x, int n, int c,
+                                                             int hw, const float* __restrict__ absmax,
+                                                             int8_t* __restrict__ out, long long plane) {
+  const float qmax = act_qmax<L>();
+  const long long total = (long long)n * hw;
+  for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < total;
+       p += (long long)gridDim.x * blockDim.x) {
+    const int img = (int)(p / hw);
+    const int pix = (int)(p - (long long)img * hw);
+    const float am = absmax[img];
+    const float inv = am > 0.f ? qmax / am : 0.f;
+    unsigned int word[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) word[l] = 0u;
+    for (int ch = 0; ch < c; ++ch) {
+      const float v = x[((size_t)img * c + ch) * hw + pix];
+      float qf = fminf(fmaxf(rintf(v * inv), -qmax), qmax);
+      int d[L];
+      split_limbs<L>((int)qf, d);
+#pragma unroll
+      for (int l = 0; l < L; ++l) word[l] |= (unsigned int)(d[l] & 255) << (8 * ch);
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l) *reinterpret_cast<unsigned int*>(out + l * plane + 4 * p) = word[l];
+  }
+}
+
+// 3x3 / stride 2 / pad 1 max pool (resnet.py:147) on NHWC fp32, fused with the activation
+// quantizer of its output (per-image range absmax = max of the pool input: max-pooling a
+// non-negative ReLU output keeps the per-image maximum). Optional fp32 output.
+// One thread = 4 channels of one output pixel.
+template <int L>
+__global__ __launch_bounds__(256) void maxpool_quantize_kernel(const float* __restrict__ x, int n, int h,
+                                                               int w, int c, int ho, int wo,
+                                                               const float* __restrict__ absmax,
+                                                               int8_t* __restrict__ out, long long plane,
+                                                               float* __restrict__ out_f32) {
+  const float qmax = act_qmax<L>();
+  const int c4 = c / 4;
+  const long long total = (long long)n * ho * wo * c4;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int cq = (int)(t % c4);
+    long long p = t / c4;
+    const int ow = (int)(p % wo);
+    p /= wo;
+    const int oh = (int)(p % ho);
+    const int img = (int)(p / ho);
+    float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+#pragma unroll
+    for (int dr = 0; dr < 3; ++dr) {
+      const int ih = 2 * oh - 1 + dr;
+      if ((unsigned)ih >= (unsigned)h) continue;
+#pragma unroll
+      for (int dc = 0; dc < 3; ++dc) {
+        const int iw = 2 * ow - 1 + dc;
+        if ((unsigned)iw >= (unsigned)w) continue;
+        const float4 v = *reinterpret_cast<const float4*>(x + (((size_t)img * h + ih) * w + iw) * c + 4 * cq);
+        m.x = fmaxf(m.x, v.x);
+        m.y = fmaxf(m.y, v.y);
+        m.z = fmaxf(m.z, v.z);
+        m.w = fmaxf(m.w, v.w);
+      }
+    }
+    const size_t o = (((size_t)img * ho + oh) * wo + ow) * c + 4 * cq;
+    if (out_f32) *reinterpret_cast<float4*>(out_f32 + o) = m;
+    const float am = absmax[img];
+    const float inv = am > 0.f ? qmax / am : 0.f;
+    const float vals[4] = {m.x, m.y, m.z, m.w};
+    unsigned int word[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) word[l] = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float qf = fminf(fmaxf(rintf(vals[k] * inv), -qmax), qmax);
+      int d[L];
+      split_limbs<L>((int)qf, d);
+#pragma unroll
+      for (int l = 0; l < L; ++l) word[l] |= (unsigned int)(d[l] & 255) << (8 * k);
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l) *reinterpret_cast<unsigned int*>(out + l * plane + o) = word[l];
+  }
+}
+
 __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, int64_t per_image,
                                                      float* __restrict__ out) {
   const int img = blockIdx.y;
@@ -405,7 +575,7 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x
       m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
   } else {
-    for (int64_t i = start / 4 + 0; i < per_image; i += stride / 4) m = fmaxf(m, fabsf(p[i]));
+    for (int64_t i = start / 4; i < per_image; i += stride / 4) m = fmaxf(m, fabsf(p[i]));
   }
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0 && m > 0.f) atomic_max_nonneg(&out[img], m);
@@ -422,20 +592,21 @@ __global__ void debug_mfma_kernel(const int8_t* a, const int8_t* b, int32_t* c) 
   for (int r = 0; r < 4; ++r) c[(4 * (lane >> 4) + r) * 16 + frow] = acc[r];
 }
 
-template <int L, int WAVES_M, int WAVES_N, int WM, int WN, int MINW>
+// ------------------------------------------------------------------------------------------
+template <int L, int LW, bool SMALLC, int WAVES_M, int WAVES_N, int WM, int WN, int MINW>
 static int launch(const ConvArgs& a, hipStream_t stream) {
-  if constexpr (L * WM * WN * 4 > 128) {
+  if constexpr ((L + LW - 1) * WM * WN * 4 > 128) {
     // more than 128 accumulator registers per lane: not instantiated (would spill)
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: tile config too large for this limb count");
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: tile config too large for these limb counts");
   } else {
-  constexpr int BM = 16 * WM * WAVES_M, BN = 16 * WN * WAVES_N;
-  const long mt = (a.M + BM - 1) / BM;
-  const long nt = (a.cout + BN - 1) / BN;
-  const long blocks = mt * nt;
-  if (blocks > 0x7fffffffL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
-  hipLaunchKernelGGL((qconv_kernel<L, WAVES_M, WAVES_N, WM, WN, MINW>), dim3((unsigned)blocks),
-                     dim3(64 * WAVES_M * WAVES_N), 0, stream, a);
-  return check_hip(hipGetLastError(), "qconv_kernel launch");
+    constexpr int BM = 16 * WM * WAVES_M, BN = 16 * WN * WAVES_N;
+    const long mt = (a.M + BM - 1) / BM;
+    const long nt = (a.cout + BN - 1) / BN;
+    const long blocks = mt * nt;
+    if (blocks > 0x7fffffffL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
+    hipLaunchKernelGGL((qconv_kernel<L, LW, SMALLC, WAVES_M, WAVES_N, WM, WN, MINW>), dim3((unsigned)blocks),
+                       dim3(64 * WAVES_M * WAVES_N), 0, stream, a);
+    return check_hip(hipGetLastError(), "qconv_kernel launch");
   }
 }
 
@@ -453,44 +624,65 @@ constexpr TileCfg kTileCfgs[] = {
 };
 constexpr int kNumTileCfgs = sizeof(kTileCfgs) / sizeof(kTileCfgs[0]);
 
-template <int L>
-static int launch_cfg(int cfg, const ConvArgs& a, hipStream_t s) {
+template <int L, int LW>
+static int launch_cfg(int cfg, bool smallc, const ConvArgs& a, hipStream_t s) {
+  if (smallc) {
+    if constexpr (LW >= 2 && L >= 2) {
+      switch (cfg) {
+        case 2: return launch<L, LW, true, 2, 2, 4, 2, 2>(a, s);
+        case 3: return launch<L, LW, true, 2, 2, 2, 2, 4>(a, s);
+        default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: cin==4 supports tile configs 2, 3");
+      }
+    } else {
+      return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: cin==4 needs 2 weight limbs and >= 2 activation limbs");
+    }
+  }
   switch (cfg) {
-    case 0: return launch<L, 2, 2, 4, 4, 2>(a, s);
-    case 1: return launch<L, 2, 2, 2, 4, 2>(a, s);
-    case 2: return launch<L, 2, 2, 4, 2, 2>(a, s);
-    case 3: return launch<L, 2, 2, 2, 2, 4>(a, s);
-    case 4: return launch<L, 2, 4, 4, 2, 4>(a, s);
-    case 5: return launch<L, 4, 2, 2, 4, 2>(a, s);
+    case 0: return launch<L, LW, false, 2, 2, 4, 4, 2>(a, s);
+    case 1: return launch<L, LW, false, 2, 2, 2, 4, 2>(a, s);
+    case 2: return launch<L, LW, false, 2, 2, 4, 2, 2>(a, s);
+    case 3: return launch<L, LW, false, 2, 2, 2, 2, 4>(a, s);
+    case 4: return launch<L, LW, false, 2, 4, 4, 2, 2>(a, s);
+    case 5: return launch<L, LW, false, 4, 2, 2, 4, 2>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   }
 }
 
 // Default tile when the caller does not pass one (the Python layer autotunes per shape).
-static int heuristic_cfg(int L, long M, int cout, int K) {
+static int heuristic_cfg(int nacc, long M, int cout, int K, bool smallc) {
+  if (nacc >= 4) return 3;
+  if (smallc) return 2;
   if (cout <= 64) return M >= 128L * 512 ? 2 : 3;
-  if (L == 3) return K <= 256 ? 3 : 2;
+  if (nacc >= 3) return 3;
   if (K <= 256) return 1;
-  return 0;
+  return 5;
 }
 
 }  // namespace smpq
 
 using namespace smpq;
 
-extern "C" int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
-                               const int8_t* codes, const int32_t* offset, int cout, int kh, int kw,
-                               int stride, int pad, const float* col_scale, const float* col_shift,
-                               const float* residual, int relu, int limbs, float* y, float* y_absmax,
-                               int tile_cfg, smpq_stream_t stream) {
-  if (!xq || !x_absmax || !codes || !col_scale || !col_shift || !y)
+extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+                                 const int8_t* codes, int wlimbs, const int32_t* offset, int cout, int kh,
+                                 int kw, int stride, int pad, const float* col_scale,
+                                 const float* col_shift, const float* residual, int relu, int limbs,
+                                 float* y, float* y_absmax, int8_t* yq, float yq_range, int32_t* overflow,
+                                 int tile_cfg, smpq_stream_t stream) {
+  if (!xq || !x_absmax || !codes || !col_scale || !col_shift || (!y && !yq))
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: null pointer");
+  if (yq && (!overflow || !(yq_range > 0.f)))
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: yq needs overflow flag and a positive range");
+  if (yq && (cout & 3) != 0) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: yq needs cout % 4 == 0");
   if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || stride <= 0 ||
       pad < 0)
     return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: bad shape");
-  if (cin % kKStep != 0)
-    return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: cin must be a multiple of 64 (got " +
+  const bool smallc = cin == 4;
+  if (!smallc && cin % kKStep != 0)
+    return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: cin must be 4 or a multiple of 64 (got " +
                                   std::to_string(cin) + ")");
+  if (wlimbs < 1 || wlimbs > 3) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: wlimbs must be 1, 2 or 3");
+  if (wlimbs == 3 && limbs != 3)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: 3 weight limbs are built for 3 activation limbs only");
   ConvArgs a;
   a.xq = xq;
   a.plane = (long long)n * h * w * cin;
@@ -502,6 +694,9 @@ extern "C" int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, i
   a.residual = residual;
   a.y = y;
   a.y_absmax = y_absmax;
+  a.yq = yq;
+  a.overflow = overflow;
+  a.yq_inv = yq ? (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f)) / yq_range : 0.f;
   a.n = n;
   a.h = h;
   a.w = w;
@@ -518,27 +713,57 @@ extern "C" int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, i
   if (M > 0x7fffffffL || a.plane > 0x7fffffffLL * 8 || (long)n * h * w > 0x7fffffffL)
     return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: tensor too large");
   a.M = (int)M;
-  a.K = kh * kw * cin;
-  a.cchunks = cin / kKStep;
-  a.ksteps = kh * kw * a.cchunks;
-  a.relu = relu ? 1 : 0;
-  a.has_offset = offset ? 1 : 0;
-  hipStream_t s = (hipStream_t)stream;
-  if (tile_cfg < 0) tile_cfg = heuristic_cfg(limbs, M, cout, a.K);
-  if (tile_cfg >= kNumTileCfgs) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
-  switch (limbs) {
-    case 1:
-      a.inv_qmax = 1.f / 127.f;
-      return launch_cfg<1>(tile_cfg, a, s);
-    case 2:
-      a.inv_qmax = 1.f / 32512.f;
-      return launch_cfg<2>(tile_cfg, a, s);
-    case 3:
-      a.inv_qmax = 1.f / 8323072.f;
-      return launch_cfg<3>(tile_cfg, a, s);
-    default:
-      return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: limbs must be 1, 2 or 3");
+  if (smallc) {
+    const int taps = kh * kw;
+    a.ksteps = (taps + 15) / 16;
+    a.K = a.ksteps * kKStep;
+    a.cchunks = 1;
+  } else {
+    a.K = kh * kw * cin;
+    a.cchunks = cin / kKStep;
+    a.ksteps = kh * kw * a.cchunks;
   }
+  a.wplane = (long long)cout * a.K;
+  a.relu = relu ? 1 : 0;
+  a.has_offset = (offset && wlimbs == 1) ? 1 : 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (tile_cfg < 0) tile_cfg = heuristic_cfg(limbs + wlimbs - 1, M, cout, a.K, smallc);
+  if (tile_cfg >= kNumTileCfgs) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
+  if (limbs < 1 || limbs > 3) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: limbs must be 1, 2 or 3");
+  a.inv_qmax = 1.f / (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f));
+  if (wlimbs == 1) {
+    switch (limbs) {
+      case 1: return launch_cfg<1, 1>(tile_cfg, smallc, a, s);
+      case 2: return launch_cfg<2, 1>(tile_cfg, smallc, a, s);
+      default: return launch_cfg<3, 1>(tile_cfg, smallc, a, s);
+    }
+  }
+  if (wlimbs == 3) return launch_cfg<3, 3>(tile_cfg, smallc, a, s);
+  switch (limbs) {
+    case 1: return launch_cfg<1, 2>(tile_cfg, smallc, a, s);
+    case 2: return launch_cfg<2, 2>(tile_cfg, smallc, a, s);
+    default: return launch_cfg<3, 2>(tile_cfg, smallc, a, s);
+  }
+}
+
+extern "C" int smpq_conv2d_fwd_ex(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+                                  const int8_t* codes, int wlimbs, const int32_t* offset, int cout, int kh,
+                                  int kw, int stride, int pad, const float* col_scale,
+                                  const float* col_shift, const float* residual, int relu, int limbs,
+                                  float* y, float* y_absmax, int tile_cfg, smpq_stream_t stream) {
+  if (!y) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: null pointer");
+  return smpq_conv2d_fwd_q(xq, x_absmax, n, h, w, cin, codes, wlimbs, offset, cout, kh, kw, stride, pad,
+                           col_scale, col_shift, residual, relu, limbs, y, y_absmax, nullptr, 0.f, nullptr,
+                           tile_cfg, stream);
+}
+
+extern "C" int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+                               const int8_t* codes, const int32_t* offset, int cout, int kh, int kw,
+                               int stride, int pad, const float* col_scale, const float* col_shift,
+                               const float* residual, int relu, int limbs, float* y, float* y_absmax,
+                               int tile_cfg, smpq_stream_t stream) {
+  return smpq_conv2d_fwd_ex(xq, x_absmax, n, h, w, cin, codes, 1, offset, cout, kh, kw, stride, pad,
+                            col_scale, col_shift, residual, relu, limbs, y, y_absmax, tile_cfg, stream);
 }
 
 extern "C" int smpq_conv2d_num_tile_configs(void) { return kNumTileCfgs; }
@@ -553,36 +778,66 @@ extern "C" int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads) 
   return SMPQ_OK;
 }
 
+extern "C" size_t smpq_conv2d_workspace_bytes(int, int, int, int, int, int, int, int, int, int) {
+  return 0;
+}
+
+static long long grid_for(long long work) {
+  long long blocks = (work + 255) / 256;
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  if (blocks < 1) blocks = 1;
+  return blocks;
+}
+
 extern "C" int smpq_act_quantize(const float* x, int n, int64_t per_image, const float* absmax, int limbs,
                                  int8_t* out, smpq_stream_t stream) {
   if (!x || !absmax || !out || n <= 0 || per_image <= 0)
     return fail(SMPQ_E_INVALID, "smpq_act_quantize: bad arguments");
   if (per_image % 8 != 0) return fail(SMPQ_E_SHAPE, "smpq_act_quantize: per_image % 8 != 0");
   const long long total = (long long)n * per_image;
-  long long blocks = (total / 8 + 255) / 256;
-  if (blocks > 256 * 16) blocks = 256 * 16;
+  const dim3 grid((unsigned)grid_for(total / 8));
   hipStream_t s = (hipStream_t)stream;
   switch (limbs) {
-    case 1:
-      hipLaunchKernelGGL(act_quantize_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, x, total, per_image,
-                         absmax, 127.f, out, total);
-      break;
-    case 2:
-      hipLaunchKernelGGL(act_quantize_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, x, total, per_image,
-                         absmax, 32512.f, out, total);
-      break;
-    case 3:
-      hipLaunchKernelGGL(act_quantize_kernel<3>, dim3((unsigned)blocks), dim3(256), 0, s, x, total, per_image,
-                         absmax, 8323072.f, out, total);
-      break;
-    default:
-      return fail(SMPQ_E_INVALID, "smpq_act_quantize: limbs must be 1, 2 or 3");
+    case 1: hipLaunchKernelGGL(act_quantize_kernel<1>, grid, dim3(256), 0, s, x, total, per_image, absmax, out, total); break;
+    case 2: hipLaunchKernelGGL(act_quantize_kernel<2>, grid, dim3(256), 0, s, x, total, per_image, absmax, out, total); break;
+    case 3: hipLaunchKernelGGL(act_quantize_kernel<3>, grid, dim3(256), 0, s, x, total, per_image, absmax, out, total); break;
+    default: return fail(SMPQ_E_INVALID, "smpq_act_quantize: limbs must be 1, 2 or 3");
   }
   return check_hip(hipGetLastError(), "act_quantize_kernel launch");
 }
 
-extern "C" size_t smpq_conv2d_workspace_bytes(int, int, int, int, int, int, int, int, int, int) {
-  return 0;
+extern "C" int smpq_image_quantize(const float* x, int n, int c, int h, int w, const float* absmax, int limbs,
+                                   int8_t* out, smpq_stream_t stream) {
+  if (!x || !absmax || !out || n <= 0 || c <= 0 || c > 4 || h <= 0 || w <= 0)
+    return fail(SMPQ_E_INVALID, "smpq_image_quantize: bad arguments");
+  const long long hw = (long long)h * w;
+  const long long plane = (long long)n * hw * 4;
+  const dim3 grid((unsigned)grid_for((long long)n * hw));
+  hipStream_t s = (hipStream_t)stream;
+  switch (limbs) {
+    case 1: hipLaunchKernelGGL(image_quantize_kernel<1>, grid, dim3(256), 0, s, x, n, c, (int)hw, absmax, out, plane); break;
+    case 2: hipLaunchKernelGGL(image_quantize_kernel<2>, grid, dim3(256), 0, s, x, n, c, (int)hw, absmax, out, plane); break;
+    case 3: hipLaunchKernelGGL(image_quantize_kernel<3>, grid, dim3(256), 0, s, x, n, c, (int)hw, absmax, out, plane); break;
+    default: return fail(SMPQ_E_INVALID, "smpq_image_quantize: limbs must be 1, 2 or 3");
+  }
+  return check_hip(hipGetLastError(), "image_quantize_kernel launch");
+}
+
+extern "C" int smpq_maxpool_quantize(const float* x, int n, int h, int w, int c, const float* absmax, int limbs,
+                                     int8_t* out, float* out_f32, smpq_stream_t stream) {
+  if (!x || !absmax || !out || n <= 0 || h <= 0 || w <= 0 || c <= 0 || c % 4 != 0)
+    return fail(SMPQ_E_INVALID, "smpq_maxpool_quantize: bad arguments");
+  const int ho = (h + 2 - 3) / 2 + 1, wo = (w + 2 - 3) / 2 + 1;
+  const long long plane = (long long)n * ho * wo * c;
+  const dim3 grid((unsigned)grid_for(plane / 4));
+  hipStream_t s = (hipStream_t)stream;
+  switch (limbs) {
+    case 1: hipLaunchKernelGGL(maxpool_quantize_kernel<1>, grid, dim3(256), 0, s, x, n, h, w, c, ho, wo, absmax, out, plane, out_f32); break;
+    case 2: hipLaunchKernelGGL(maxpool_quantize_kernel<2>, grid, dim3(256), 0, s, x, n, h, w, c, ho, wo, absmax, out, plane, out_f32); break;
+    case 3: hipLaunchKernelGGL(maxpool_quantize_kernel<3>, grid, dim3(256), 0, s, x, n, h, w, c, ho, wo, absmax, out, plane, out_f32); break;
+    default: return fail(SMPQ_E_INVALID, "smpq_maxpool_quantize: limbs must be 1, 2 or 3");
+  }
+  return check_hip(hipGetLastError(), "maxpool_quantize_kernel launch");
 }
 
 extern "C" int smpq_act_absmax(const float* x, int n, int64_t per_image, float* absmax,

@@ -73,62 +73,100 @@ __global__ __launch_bounds__(kQThreads) void quantize_channels_kernel(
   if (threadIdx.x == 0) scale_out[c] = s32;
 }
 
-// Codes m = rne(w / step) (exact: w = fl32(m * step) with |m| <= 2^9 so |w/step - m| < 2^-14),
-// verified bitwise against fl32(m * step); stored as m - offset in the conv's K order
-// [kh][kw][cin] so one 64-wide K step is 64 contiguous input channels of one tap (NHWC).
-__global__ __launch_bounds__(kQThreads) void pack_weights_kernel(
-    const float* __restrict__ w, int cin, int kh, int kw, const float* __restrict__ step,
-    int8_t* __restrict__ codes, int32_t* __restrict__ offset, int32_t* __restrict__ status) {
-  __shared__ int smem[3 * kQThreads / kWave];
+// Weight codes for the conv's B operand, one workgroup per output channel.
+//   w [cout][cin][kh][kw] fp32, step [cout] (0 = channel never quantized).
+//   Exact mode (step > 0 and every w == fl32(m * step), |m| <= WMAX): the integer codes m of
+//     the reference quantizer (functions.py:41) — recovered by m = rne(w / step), exact because
+//     |w / step - m| < 2^-14 — verified bitwise.
+//   Fixed mode (lw >= 2: unquantized / off-grid channels): per-channel fixed point with
+//     WMAX = 32512 (lw 2, 16-bit) or 8323072 (lw 3, 24-bit): wscale = max|w| / WMAX,
+//     m = rne(w / wscale).
+//   lw == 1: m - offset stored as one int8 plane (offset != 0 only when [min m, max m] is not
+//     inside [-128, 127]); lw >= 2: m stored as lw balanced int8 digit planes, no offset.
+//   Layout: codes[l][c][k], k = tap * cin_pad + ci (tap = r * kw + q), zero-padded to K.
+//   status[0] += off-grid channels (lw == 1: error), status[1] += channels whose exact codes do
+//   not fit (lw == 1: > 256 levels), status[2] += channels coded in fixed mode.
+constexpr float kW16Max = 32512.f;    // 2-limb fixed-point code range (127 * 256)
+constexpr float kW24Max = 8323072.f;  // 3-limb fixed-point code range (127 * 65536)
+
+__global__ __launch_bounds__(kQThreads) void pack_weights_ex_kernel(
+    const float* __restrict__ w, int cin, int kh, int kw, int cin_pad, int K, int lw,
+    const float* __restrict__ step, int8_t* __restrict__ codes, long long wplane,
+    int32_t* __restrict__ offset, float* __restrict__ wscale, int32_t* __restrict__ status) {
+  __shared__ int smem[4 * kQThreads / kWave];
+  __shared__ float sabs[kQThreads / kWave];
   const int c = blockIdx.x;
   const int taps = kh * kw;
-  const int k = cin * taps;
-  const float* row = w + (size_t)c * k;
-  const float s = step[c];
-  int mmin = INT32_MAX, mmax = INT32_MIN, bad = 0;
-  for (int i = threadIdx.x; i < k; i += kQThreads) {
+  const int kreal = cin * taps;
+  const float* row = w + (size_t)c * kreal;
+  const float s = step ? step[c] : 0.f;
+  const float wmax = lw >= 3 ? kW24Max : kW16Max;
+  int mmin = INT32_MAX, mmax = INT32_MIN, bad = (s > 0.f) ? 0 : 1;
+  float amax = 0.f;
+  for (int i = threadIdx.x; i < kreal; i += kQThreads) {
     const float v = row[i];
+    amax = fmaxf(amax, fabsf(v));
+    if (bad) continue;
     const float mf = rintf(__fdiv_rn(v, s));
-    if (!(s > 0.f) || __fmul_rn(mf, s) != v || fabsf(mf) > 65536.f) {
+    if (__fmul_rn(mf, s) != v || fabsf(mf) > wmax) {
       bad = 1;
       continue;
     }
-    const int m = (int)mf;
-    mmin = min(mmin, m);
-    mmax = max(mmax, m);
+    mmin = min(mmin, (int)mf);
+    mmax = max(mmax, (int)mf);
   }
   mmin = wave_min_i(mmin);
   mmax = wave_max_i(mmax);
   bad = wave_max_i(bad);
+  amax = wave_max(amax);
   const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   if (lane == 0) {
     smem[wid] = mmin;
     smem[4 + wid] = mmax;
     smem[8 + wid] = bad;
+    sabs[wid] = amax;
   }
   __syncthreads();
   mmin = min(min(smem[0], smem[1]), min(smem[2], smem[3]));
   mmax = max(max(smem[4], smem[5]), max(smem[6], smem[7]));
   bad = smem[8] | smem[9] | smem[10] | smem[11];
+  amax = fmaxf(fmaxf(sabs[0], sabs[1]), fmaxf(sabs[2], sabs[3]));
   int o = 0;
-  bool range_bad = false;
-  if (!bad) {
-    if (mmax - mmin > 255) range_bad = true;
-    else if (mmin < -128 || mmax > 127) o = mmin + 128;
+  bool fixed = false, range_bad = false;
+  float sc = s;
+  if (lw == 1) {
+    if (!bad) {
+      if (mmax - mmin > 255) range_bad = true;
+      else if (mmin < -128 || mmax > 127) o = mmin + 128;
+    }
+  } else if (bad) {
+    fixed = true;
+    sc = amax > 0.f ? amax / wmax : 1.f;
   }
   if (threadIdx.x == 0) {
-    if (bad) atomicAdd(&status[0], 1);
+    if (bad && s > 0.f) atomicAdd(&status[0], 1);
+    if (lw == 1 && bad && !(s > 0.f)) atomicAdd(&status[0], 1);
     if (range_bad) atomicAdd(&status[1], 1);
-    offset[c] = o;
+    if (fixed) atomicAdd(&status[2], 1);
+    if (offset) offset[c] = o;
+    if (wscale) wscale[c] = sc;
   }
-  int8_t* out = codes + (size_t)c * k;
-  for (int i = threadIdx.x; i < k; i += kQThreads) {
-    // reference order i = (ci*kh + r)*kw + q ; kernel order j = (r*kw + q)*cin + ci
-    const int ci = i / taps;
-    const int t = i - ci * taps;
+  const bool zero = (lw == 1) && (bad || range_bad);
+  for (int k = threadIdx.x; k < K; k += kQThreads) {
+    const int tap = k / cin_pad;
+    const int ci = k - tap * cin_pad;
     int m = 0;
-    if (!bad && !range_bad) m = (int)rintf(__fdiv_rn(row[i], s)) - o;
-    out[(size_t)t * cin + ci] = (int8_t)m;
+    if (!zero && tap < taps && ci < cin) {
+      const float v = row[ci * taps + tap];
+      // fixed point: round in double (at 24 bits an fp32 quotient cannot round exactly)
+      if (fixed) m = (int)fmin(fmax(rint((double)v / (double)sc), -(double)wmax), (double)wmax);
+      else m = (int)rintf(__fdiv_rn(v, sc)) - o;
+    }
+    for (int l = 0; l < lw; ++l) {  // balanced base-256 digits (the last one takes the rest)
+      const int lo = (l == lw - 1) ? m : ((m + 128) & 255) - 128;
+      codes[l * wplane + (size_t)c * K + k] = (int8_t)lo;
+      m = (m - lo) >> 8;
+    }
   }
 }
 
@@ -191,7 +229,33 @@ extern "C" int smpq_pack_weights(const float* w, int cout, int cin, int kh, int 
                                  int32_t* status, smpq_stream_t stream) {
   if (!w || !step || !codes || !offset || !status || cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0)
     return fail(SMPQ_E_INVALID, "smpq_pack_weights: bad arguments");
-  hipLaunchKernelGGL(pack_weights_kernel, dim3(cout), dim3(kQThreads), 0, (hipStream_t)stream, w,
-                     cin, kh, kw, step, codes, offset, status);
-  return check_hip(hipGetLastError(), "pack_weights_kernel launch");
+  const int K = cin * kh * kw;
+  hipLaunchKernelGGL(pack_weights_ex_kernel, dim3(cout), dim3(kQThreads), 0, (hipStream_t)stream, w,
+                     cin, kh, kw, cin, K, 1, step, codes, (long long)cout * K, offset, (float*)nullptr,
+                     status);
+  return check_hip(hipGetLastError(), "pack_weights_ex_kernel launch");
+}
+
+extern "C" int smpq_pack_weights_ex(const float* w, int cout, int cin, int kh, int kw, const float* step,
+                                    int wlimbs, int8_t* codes, int32_t* offset, float* wscale,
+                                    int32_t* status, smpq_stream_t stream) {
+  if (!w || !codes || !wscale || !status || cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0)
+    return fail(SMPQ_E_INVALID, "smpq_pack_weights_ex: bad arguments");
+  if (wlimbs < 1 || wlimbs > 3) return fail(SMPQ_E_INVALID, "smpq_pack_weights_ex: wlimbs must be 1, 2 or 3");
+  if (wlimbs == 1 && (!step || !offset))
+    return fail(SMPQ_E_INVALID, "smpq_pack_weights_ex: wlimbs == 1 needs step and offset");
+  int cin_pad, K;
+  if (cin <= 4) {
+    cin_pad = 4;
+    K = ((kh * kw + 15) / 16) * 64;
+  } else if (cin % 64 == 0) {
+    cin_pad = cin;
+    K = cin * kh * kw;
+  } else {
+    return fail(SMPQ_E_SHAPE, "smpq_pack_weights_ex: cin must be <= 4 or a multiple of 64");
+  }
+  hipLaunchKernelGGL(pack_weights_ex_kernel, dim3(cout), dim3(kQThreads), 0, (hipStream_t)stream, w,
+                     cin, kh, kw, cin_pad, K, wlimbs, step, codes, (long long)cout * K, offset, wscale,
+                     status);
+  return check_hip(hipGetLastError(), "pack_weights_ex_kernel launch");
 }

@@ -40,8 +40,15 @@ _PROTOS = {
     "smpq_pack_weights": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "smpq_act_absmax": (_i, [_vp, _i, _i64, _vp, _vp]),
     "smpq_act_quantize": (_i, [_vp, _i, _i64, _vp, _i, _vp, _vp]),
+    "smpq_pack_weights_ex": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
+    "smpq_image_quantize": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
+    "smpq_maxpool_quantize": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp]),
+    "smpq_conv2d_fwd_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp,
+                                _vp, _i, _i, _vp, _vp, _i, _vp]),
     "smpq_conv2d_fwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp,
                              _vp, _i, _i, _vp, _vp, _i, _vp]),
+    "smpq_conv2d_fwd_q": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp,
+                               _vp, _i, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _i, _vp]),
     "smpq_conv2d_num_tile_configs": (_i, []),
     "smpq_conv2d_tile_config": (_i, [_i, _vp, _vp, _vp]),
     "smpq_conv2d_workspace_bytes": (ctypes.c_size_t, [_i] * 10),

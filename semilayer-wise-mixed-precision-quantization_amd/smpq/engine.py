@@ -1,24 +1,64 @@
-"""Fused eval-mode ResNet forward on the HIP path (NHWC end to end).
+"""Fused eval-mode ResNet forward, every conv on the HIP path (NHWC end to end).
 
 Restates ``ResNet._forward_impl`` (resnet.py:204-220), ``BasicBlock.forward`` (resnet.py:55-68)
-and ``Bottleneck.forward`` (resnet.py:97-116) with every quantized conv + its BatchNorm
-(+ residual add) (+ ReLU) as ONE ``smpq_conv2d_fwd`` launch:
+and ``Bottleneck.forward`` (resnet.py:97-116):
 
-  * activations stay NHWC fp32 in HBM between layers (no layout round trips);
-  * each conv epilogue also produces the per-image max|y| that the NEXT conv's activation
-    quantizer needs (atomicMax), so there is no separate range pass;
-  * BN (eval) is folded per output channel: a = gamma / sqrt(var + eps), b = beta - mean * a,
-    and the weight step is folded into the same column scale.
+  * input: per-image range + quantization of the NCHW image into 4-channel NHWC limb planes
+    (``image_quantize``);
+  * stem conv 7x7/2 + BN + ReLU (resnet.py:143-146) = one ``conv2d_q`` launch (fp32 weights as
+    2 int8 limbs), then MaxPool 3x3/2 fused with the quantization of its output
+    (``maxpool_quantize``);
+  * every block conv + its BN (+ residual add) (+ ReLU) = one ``conv2d_q`` launch whose
+    epilogue also yields the per-image max|y| the NEXT conv's activation quantizer needs;
+  * the downsample 1x1 conv + BN (resnet.py:188-192) reads the block input's limb planes
+    (already quantized for conv1) and writes the fp32 identity consumed by conv3's epilogue;
+  * avgpool + fc (resnet.py:216-218) stay torch ops (2 MMAC/image).
 
-Unquantized parts stay fp32 exactly like the reference: the 7x7 stem + BN + ReLU + maxpool,
-the downsample 1x1 conv + BN (resnet.py:188-192), avgpool and fc run as torch/MIOpen ops on
-channels_last tensors, as does any conv that is not fully quantized (see qconv.py).
+An activation is carried as ``Act`` = fp32 NHWC tensor and/or its int8 limb planes plus its
+per-image range; limb planes are produced at most once per activation.
+
+Range modes (``set_range_mode``):
+  * "dynamic": every activation's range is its per-image max|x| (from the producer's epilogue),
+    the producer writes fp32 and ``act_quantize`` makes the limb planes — each image's result is
+    independent of the batch;
+  * "static" (default): per-layer ranges calibrated by a dynamic forward (max over the batch x
+    ``HEADROOM``); each conv's epilogue writes the NEXT conv's limb planes directly (no fp32 for
+    block-internal tensors, no quantize pass). A value beyond its range sets an overflow flag
+    and the forward is recomputed in dynamic mode, widening the ranges, so results are never
+    silently clamped. Calibration is redone whenever a weight, BN buffer or the limb count changes.
 """
 import torch
 import torch.nn.functional as F
 
 from . import ops
 from .qconv import QConv2d, stats
+
+_MODE = ["static"]
+HEADROOM = 2.0
+stats.setdefault("calibrations", 0)
+stats.setdefault("overflow_reruns", 0)
+
+
+def set_range_mode(mode):
+    if mode not in ("static", "dynamic"):
+        raise ValueError("range mode must be 'static' or 'dynamic'")
+    _MODE[0] = mode
+
+
+def get_range_mode():
+    return _MODE[0]
+
+
+class Act:
+    __slots__ = ("f32", "q", "amax")
+
+    def __init__(self, f32=None, q=None, amax=None):
+        self.f32, self.q, self.amax = f32, q, amax
+
+    def limbs(self):
+        if self.q is None:
+            self.q = ops.act_quantize(self.f32, self.amax)
+        return self.q
 
 
 def _bn_fold(bn):
@@ -29,6 +69,8 @@ def _bn_fold(bn):
 
 
 def _bn_key(bn):
+    if bn is None:
+        return None
     ts = [bn.running_mean, bn.running_var]
     if bn.affine:
         ts += [bn.weight, bn.bias]
@@ -36,23 +78,26 @@ def _bn_key(bn):
 
 
 def conv_plan(conv, bn):
-    """(codes, offset, col_scale, col_shift) for the fused kernel, or None (fp32 path)."""
+    """(codes, offset, col_scale, col_shift, kind) for the fused kernel, or None."""
     if not isinstance(conv, QConv2d):
-        return None
-    if conv.stride[0] != conv.stride[1] or conv.padding[0] != conv.padding[1] or conv.bias is not None:
         return None
     pk = conv.packed()
     if pk is None:
         return None
-    key = (conv._pack_key(), _bn_key(bn))
+    key = (conv._pack_key(), _bn_key(bn), None if conv.bias is None else (conv.bias.data_ptr(), conv.bias._version))
     cache = getattr(conv, "_fold_cache", None)
     if cache is not None and cache[0] == key:
         return cache[1]
+    codes, _, offset, wscale, kind = pk
     with torch.no_grad():
-        a, b = _bn_fold(bn)
-        col_scale = (conv.qstep.float() * a).contiguous()
-        col_shift = b.contiguous()
-    plan = (pk[0], pk[1], col_scale, col_shift)
+        if bn is not None:
+            a, b = _bn_fold(bn)
+        else:
+            a = torch.ones_like(wscale)
+            b = torch.zeros_like(wscale)
+        if conv.bias is not None:
+            b = b + conv.bias.float() * a
+        plan = (codes, offset, (wscale * a).contiguous(), b.contiguous(), kind)
     conv._fold_cache = (key, plan)
     return plan
 
@@ -65,75 +110,155 @@ def _to_nhwc(x):
     return x.permute(0, 2, 3, 1).contiguous()
 
 
-def conv_bn_act(conv, bn, x, x_amax, relu, residual=None, y_amax=None):
-    """y = act(bn(conv(x)) [+ residual]) on NHWC fp32; fills y_amax (per image max|y|) if given."""
+class Ctx:
+    """Per-forward state: range mode, calibrated ranges, recorded maxima, overflow flag."""
+
+    def __init__(self, n, device, ranges=None, record=False):
+        self.n, self.device = n, device
+        self.ranges = ranges            # {id(conv): range} (static mode) or None
+        self.record = {} if record else None
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=device) if ranges else None
+        self._rt = {}
+
+    def range_tensor(self, conv):
+        t = self._rt.get(id(conv))
+        if t is None:
+            t = torch.full((self.n,), self.ranges[id(conv)], dtype=torch.float32, device=self.device)
+            self._rt[id(conv)] = t
+        return t
+
+
+def run_conv(conv, bn, act, relu, residual=None, want_amax=True, ctx=None, want_f32=True):
+    """y = act(bn(conv(x)) [+ residual]) -> Act (NHWC fp32 and/or the next conv's limb planes)."""
+    n = act.amax.shape[0] if act.amax is not None else act.f32.shape[0]
     plan = conv_plan(conv, bn)
+    static = ctx is not None and ctx.ranges is not None and want_amax and plan is not None \
+        and id(conv) in ctx.ranges and conv.out_channels % 4 == 0
+    yam = torch.zeros(n, dtype=torch.float32, device=conv.weight.device) if (want_amax and not static) else None
     if plan is not None:
-        codes, offset, col_scale, col_shift = plan
+        codes, offset, col_scale, col_shift, kind = plan
         stats["hip_conv"] += 1
-        conv.last_path = "hip"
-        return ops.conv2d_nhwc(x, x_amax, codes, offset, conv.kernel_size[0], conv.kernel_size[1],
+        if kind == "fixed":
+            stats["fixed_conv"] += 1
+        conv.last_path = "hip-" + kind
+        if static:
+            rng = ctx.ranges[id(conv)]
+            y, yq = ops.tuned_conv2d_q(act.limbs(), act.amax, codes, offset, conv.kernel_size[0],
+                                       conv.kernel_size[1], conv.stride[0], conv.padding[0], col_scale, col_shift,
+                                       residual=residual, relu=relu, emit_range=rng, overflow=ctx.overflow,
+                                       want_f32=want_f32)
+            return Act(f32=y, q=yq, amax=ctx.range_tensor(conv))
+        y = ops.tuned_conv2d_q(act.limbs(), act.amax, codes, offset, conv.kernel_size[0], conv.kernel_size[1],
                                conv.stride[0], conv.padding[0], col_scale, col_shift,
-                               residual=residual, relu=relu, y_absmax=y_amax)
-    # fp32 path (unquantized weights: the reference's own arithmetic, on MIOpen)
+                               residual=residual, relu=relu, y_absmax=yam)
+        if ctx is not None and ctx.record is not None and yam is not None:
+            ctx.record[id(conv)] = yam
+        return Act(f32=y, amax=yam)
+    yam = torch.zeros(n, dtype=torch.float32, device=conv.weight.device) if want_amax else None
+    # geometry the kernel does not cover: the reference's fp32 arithmetic on MIOpen
     stats["fp32_conv"] += 1
     conv.last_path = "fp32"
-    y = F.conv2d(_to_nchw(x), conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups)
-    y = F.batch_norm(y, bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
+    y = F.conv2d(_to_nchw(act.f32), conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups)
+    if bn is not None:
+        y = F.batch_norm(y, bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
     if residual is not None:
         y = y + _to_nchw(residual)
     if relu:
         y = F.relu(y)
     y = _to_nhwc(y)
-    if y_amax is not None:
-        ops.act_absmax(y, out=y_amax)
-    return y
+    if want_amax:
+        ops.act_absmax(y, out=yam)
+    return Act(f32=y, amax=yam)
 
 
-def _downsample(ds, x):
-    conv, bn = ds[0], ds[1]
-    plan = conv_plan(conv, bn)
-    if plan is not None:
-        amax = ops.act_absmax(x)
-        return conv_bn_act(conv, bn, x, amax, relu=False)
-    y = F.conv2d(_to_nchw(x), conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups)
-    y = F.batch_norm(y, bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
-    return _to_nhwc(y)
-
-
-def block_forward(blk, x, x_amax, amax_bank, idx):
-    """One BasicBlock / Bottleneck on NHWC x. Returns (out, out_amax, next bank index)."""
-    identity = x
+def block_forward(blk, x, ctx=None, last=False):
+    """One BasicBlock / Bottleneck on an Act; returns the output Act. Block-internal activations
+    never need fp32 in static mode; the block output keeps fp32 (identity path, avgpool)."""
     if blk.downsample is not None:
-        identity = _downsample(blk.downsample, x)
+        identity = run_conv(blk.downsample[0], blk.downsample[1], x, relu=False, want_amax=False, ctx=ctx).f32
+    else:
+        identity = x.f32
+    out_amax = not last  # the last block feeds only avgpool
     if hasattr(blk, "conv3"):  # Bottleneck (resnet.py:97-116)
-        t1 = conv_bn_act(blk.conv1, blk.bn1, x, x_amax, True, y_amax=amax_bank[idx])
-        t2 = conv_bn_act(blk.conv2, blk.bn2, t1, amax_bank[idx], True, y_amax=amax_bank[idx + 1])
-        out = conv_bn_act(blk.conv3, blk.bn3, t2, amax_bank[idx + 1], True, residual=identity,
-                          y_amax=amax_bank[idx + 2])
-        return out, amax_bank[idx + 2], idx + 3
+        t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
+        t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
+        return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax)
     # BasicBlock (resnet.py:55-68)
-    t1 = conv_bn_act(blk.conv1, blk.bn1, x, x_amax, True, y_amax=amax_bank[idx])
-    out = conv_bn_act(blk.conv2, blk.bn2, t1, amax_bank[idx], True, residual=identity,
-                      y_amax=amax_bank[idx + 1])
-    return out, amax_bank[idx + 1], idx + 2
+    t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
+    return run_conv(blk.conv2, blk.bn2, t1, True, residual=identity, ctx=ctx, want_amax=out_amax)
+
+
+def stem_forward(model, x):
+    """conv1 7x7/2 + bn1 + relu + maxpool 3x3/2 (resnet.py:206-209) -> Act of the pooled output."""
+    x = x.float().contiguous()
+    n = x.shape[0]
+    plan = conv_plan(model.conv1, model.bn1)
+    if plan is not None and x.shape[1] <= 4 and isinstance(model.maxpool, torch.nn.MaxPool2d) \
+            and model.maxpool.kernel_size in (3, (3, 3)) and model.maxpool.stride in (2, (2, 2)) \
+            and model.maxpool.padding in (1, (1, 1)):
+        amax_in = ops.act_absmax(x)
+        xq = ops.image_quantize(x, amax_in)
+        stem = run_conv(model.conv1, model.bn1, Act(q=xq, amax=amax_in), relu=True)
+        q, f = ops.maxpool_quantize(stem.f32, stem.amax, want_f32=True)
+        return Act(f32=f, q=q, amax=stem.amax)
+    h = model.maxpool(model.relu(model.bn1(model.conv1(x.contiguous(memory_format=torch.channels_last)))))
+    h = _to_nhwc(h)
+    amax = ops.act_absmax(h)
+    return Act(f32=h, amax=amax)
+
+
+def _blocks(model):
+    return [b for layer in (model.layer1, model.layer2, model.layer3, model.layer4) for b in layer]
+
+
+def _forward(model, x, ctx):
+    act = stem_forward(model, x)
+    blocks = _blocks(model)
+    for i, blk in enumerate(blocks):
+        act = block_forward(blk, act, ctx, last=(i == len(blocks) - 1))
+    feat = act.f32.mean(dim=(1, 2))
+    return model.fc(feat)
+
+
+def _signature(model):
+    sig = [ops.get_act_limbs(), HEADROOM]
+    for m in model.modules():
+        if isinstance(m, QConv2d):
+            sig.append(m._pack_key())
+        elif isinstance(m, torch.nn.BatchNorm2d):
+            sig.append(_bn_key(m))
+    return tuple(sig)
+
+
+def calibrate(model, x):
+    """Dynamic forward of ``x`` that (re)sets the per-layer static ranges; returns its logits."""
+    ctx = Ctx(x.shape[0], x.device, record=True)
+    y = _forward(model, x, ctx)
+    keys = list(ctx.record)
+    if keys:
+        maxima = torch.stack([ctx.record[k].amax() for k in keys]).cpu().tolist()
+        old = getattr(model, "_smpq_ranges", None)
+        ranges = {}
+        for k, v in zip(keys, maxima):
+            r = max(v, 1e-30) * HEADROOM
+            if old is not None and old[1] == _signature(model) and k in old[0]:
+                r = max(r, old[0][k])
+            ranges[k] = r
+        model._smpq_ranges = (ranges, _signature(model))
+    stats["calibrations"] += 1
+    return y
 
 
 def forward_fused(model, x):
     """Eval-mode forward of an smpq ResNet on the GPU; returns logits [n, num_classes]."""
-    x = x.float().contiguous(memory_format=torch.channels_last)
-    h = model.conv1(x)
-    h = model.bn1(h)
-    h = model.relu(h)
-    h = model.maxpool(h)
-    h = _to_nhwc(h)
-    blocks = [b for layer in (model.layer1, model.layer2, model.layer3, model.layer4) for b in layer]
-    nconv = sum(3 if hasattr(b, "conv3") else 2 for b in blocks)
-    amax_bank = torch.zeros(nconv + 1, h.shape[0], dtype=torch.float32, device=h.device)
-    ops.act_absmax(h, out=amax_bank[nconv])
-    amax = amax_bank[nconv]
-    idx = 0
-    for blk in blocks:
-        h, amax, idx = block_forward(blk, h, amax, amax_bank, idx)
-    feat = h.mean(dim=(1, 2))
-    return model.fc(feat)
+    if _MODE[0] == "dynamic":
+        return _forward(model, x, None)
+    cal = getattr(model, "_smpq_ranges", None)
+    if cal is None or cal[1] != _signature(model):
+        return calibrate(model, x)
+    ctx = Ctx(x.shape[0], x.device, ranges=cal[0])
+    y = _forward(model, x, ctx)
+    if int(ctx.overflow.item()) == 0:  # one sync: results are never silently clamped
+        return y
+    stats["overflow_reruns"] += 1
+    return calibrate(model, x)

@@ -91,7 +91,8 @@ class Bottleneck(nn.Module):
 
 
 class ResNet(nn.Module):
-    """resnet.py:119-223; stem/downsample/fc stay fp32 as in the reference."""
+    """resnet.py:119-223. The stem and downsample convs are QConv2d too (never quantized by the
+    drivers: they run with fp32 weights in 16-bit fixed point on the HIP kernel); fc stays fp32."""
 
     fused = True  # use smpq.engine on GPU in eval mode
 
@@ -111,7 +112,7 @@ class ResNet(nn.Module):
                              "got {}".format(replace_stride_with_dilation))
         self.groups = groups
         self.base_width = width_per_group
-        self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
+        self.conv1 = QConv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = norm_layer(self.inplanes)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)

@@ -84,6 +84,64 @@ def pack_weights(w, step):
     return codes, offset, status
 
 
+def pack_weights_ex(w, step, wlimbs):
+    """Weight codes for conv2d_q: (codes int8 [wlimbs, cout, K], offset int32 [cout] | None,
+    wscale fp32 [cout], status int32 [3] (device)). See include/smpq.h smpq_pack_weights_ex."""
+    _req(w.is_cuda and w.dtype == torch.float32 and w.dim() == 4, "pack_weights_ex: need a CUDA fp32 4-D weight")
+    _req(wlimbs in (1, 2, 3), "pack_weights_ex: wlimbs")
+    w = w.contiguous()
+    cout, cin, kh, kw = w.shape
+    _req(cin <= 4 or cin % 64 == 0, "pack_weights_ex: cin must be <= 4 or a multiple of 64")
+    K = ((kh * kw + 15) // 16) * 64 if cin <= 4 else cin * kh * kw
+    if step is not None:
+        step = step.to(device=w.device, dtype=torch.float32).contiguous()
+        _req(step.numel() == cout, "pack_weights_ex: step length")
+    _req(wlimbs >= 2 or step is not None, "pack_weights_ex: wlimbs=1 needs step")
+    codes = torch.empty(wlimbs, cout, K, dtype=torch.int8, device=w.device)
+    offset = torch.zeros(cout, dtype=torch.int32, device=w.device)
+    wscale = torch.empty(cout, dtype=torch.float32, device=w.device)
+    status = torch.zeros(3, dtype=torch.int32, device=w.device)
+    lib = _lib.load()
+    with torch.cuda.device(w.device):
+        _lib.check(lib.smpq_pack_weights_ex(_lib.ptr(w), cout, cin, kh, kw, _lib.ptr(step), int(wlimbs),
+                                            _lib.ptr(codes), _lib.ptr(offset), _lib.ptr(wscale), _lib.ptr(status),
+                                            _lib.stream_ptr()), "smpq_pack_weights_ex")
+    return codes, offset, wscale, status
+
+
+def image_quantize(x, x_absmax, limbs=None):
+    """NCHW fp32 images (c <= 4) -> int8 limb planes [limbs, n, h, w, 4] (stem input)."""
+    limbs = limbs or get_act_limbs()
+    _req(x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous() and x.shape[1] <= 4,
+         "image_quantize: need contiguous NCHW fp32 with <= 4 channels")
+    n, c, h, w = x.shape
+    _req(x_absmax.numel() == n and x_absmax.dtype == torch.float32, "image_quantize: absmax")
+    out = torch.empty(limbs, n, h, w, 4, dtype=torch.int8, device=x.device)
+    lib = _lib.load()
+    with torch.cuda.device(x.device):
+        _lib.check(lib.smpq_image_quantize(_lib.ptr(x), n, c, h, w, _lib.ptr(x_absmax), int(limbs), _lib.ptr(out),
+                                           _lib.stream_ptr()), "smpq_image_quantize")
+    return out
+
+
+def maxpool_quantize(x_nhwc, x_absmax, limbs=None, want_f32=True):
+    """MaxPool2d(3, 2, 1) on NHWC fp32 fused with the activation quantizer of its output.
+    Returns (limb planes [limbs, n, ho, wo, c], fp32 NHWC pooled or None)."""
+    limbs = limbs or get_act_limbs()
+    _req(x_nhwc.is_cuda and x_nhwc.dtype == torch.float32 and x_nhwc.dim() == 4 and x_nhwc.is_contiguous()
+         and x_nhwc.shape[3] % 4 == 0, "maxpool_quantize: need contiguous NHWC fp32, c % 4 == 0")
+    n, h, w, c = x_nhwc.shape
+    _req(x_absmax.numel() == n and x_absmax.dtype == torch.float32, "maxpool_quantize: absmax")
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    q = torch.empty(limbs, n, ho, wo, c, dtype=torch.int8, device=x_nhwc.device)
+    f = torch.empty(n, ho, wo, c, dtype=torch.float32, device=x_nhwc.device) if want_f32 else None
+    lib = _lib.load()
+    with torch.cuda.device(x_nhwc.device):
+        _lib.check(lib.smpq_maxpool_quantize(_lib.ptr(x_nhwc), n, h, w, c, _lib.ptr(x_absmax), int(limbs), _lib.ptr(q),
+                                             _lib.ptr(f), _lib.stream_ptr()), "smpq_maxpool_quantize")
+    return q, f
+
+
 def act_absmax(x_nhwc, out=None):
     """Per-image max|x| of an NHWC (or any [n, ...]) fp32 CUDA tensor -> fp32 [n]."""
     _req(x_nhwc.is_cuda and x_nhwc.dtype == torch.float32 and x_nhwc.is_contiguous(),
@@ -135,16 +193,25 @@ def tile_configs():
 
 
 def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
-             residual=None, relu=False, y_absmax=None, out=None, tile_cfg=-1):
-    """Quantized conv on int8 limb planes xq [L, n, h, w, cin] (from act_quantize):
-    y = conv(x, codes) * s_x * col_scale + col_shift (+res) (relu), NHWC fp32."""
+             residual=None, relu=False, y_absmax=None, out=None, tile_cfg=-1,
+             emit_range=None, overflow=None, want_f32=True):
+    """Quantized conv on int8 limb planes xq [L, n, h, w, cin] (from act_quantize / image_quantize /
+    maxpool_quantize / a previous conv2d_q) and weight limb planes codes [LW, cout, K] (or
+    [cout, K] for LW = 1): y = conv(x, w) * s_x * col_scale + col_shift (+res) (relu), NHWC fp32.
+    With ``emit_range`` (static range of the output, float) the epilogue also writes the output's
+    int8 limb planes [L, n, ho, wo, cout] and sets ``overflow`` (int32 [1]) if a value exceeded the
+    range; returns (y or None, yq) then."""
     _req(xq.is_cuda and xq.dtype == torch.int8 and xq.dim() == 5 and xq.is_contiguous(), "conv: xq must be [L,n,h,w,c] int8")
     limbs, n, h, w, cin = xq.shape
     _req(limbs in (1, 2, 3), "conv: limbs")
-    cout = codes.shape[0]
-    _req(codes.dtype == torch.int8 and codes.shape == (cout, kh * kw * cin) and codes.is_contiguous()
-         and codes.device == xq.device, "conv: codes shape")
-    _req(cin % 64 == 0, "conv: cin must be a multiple of 64")
+    if codes.dim() == 2:
+        codes = codes.unsqueeze(0)
+    wlimbs, cout, K = codes.shape
+    _req(wlimbs in (1, 2, 3) and (wlimbs < 3 or limbs == 3), "conv: weight limbs")
+    exp_k = ((kh * kw + 15) // 16) * 64 if cin == 4 else kh * kw * cin
+    _req(codes.dtype == torch.int8 and K == exp_k and codes.is_contiguous() and codes.device == xq.device,
+         "conv: codes shape")
+    _req(cin == 4 or cin % 64 == 0, "conv: cin must be 4 or a multiple of 64")
     _req(offset is None or (offset.dtype == torch.int32 and offset.numel() == cout), "conv: offset")
     _req(x_absmax.dtype == torch.float32 and x_absmax.numel() == n, "conv: x_absmax")
     for t in (col_scale, col_shift):
@@ -153,9 +220,16 @@ def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_sh
     ho = (h + 2 * pad - kh) // stride + 1
     wo = (w + 2 * pad - kw) // stride + 1
     _req(ho > 0 and wo > 0, "conv: empty output")
-    if out is None:
+    yq = None
+    if emit_range is not None:
+        _req(emit_range > 0 and cout % 4 == 0, "conv: emit_range must be > 0 and cout % 4 == 0")
+        _req(overflow is not None and overflow.dtype == torch.int32 and overflow.device == xq.device, "conv: overflow")
+        yq = torch.empty(limbs, n, ho, wo, cout, dtype=torch.int8, device=xq.device)
+    else:
+        want_f32 = True
+    if out is None and want_f32:
         out = torch.empty(n, ho, wo, cout, dtype=torch.float32, device=xq.device)
-    _req(out.shape == (n, ho, wo, cout) and out.is_contiguous(), "conv: out shape")
+    _req(out is None or (out.shape == (n, ho, wo, cout) and out.is_contiguous()), "conv: out shape")
     if residual is not None:
         _req(residual.shape == (n, ho, wo, cout) and residual.is_contiguous() and residual.dtype == torch.float32,
              "conv: residual shape")
@@ -166,12 +240,15 @@ def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_sh
     if hook is not None:
         hook.begin()
     with torch.cuda.device(xq.device):
-        _lib.check(lib.smpq_conv2d_fwd(
-            _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, cin, _lib.ptr(codes), _lib.ptr(offset), cout, kh, kw,
-            stride, pad, _lib.ptr(col_scale), _lib.ptr(col_shift), _lib.ptr(residual), 1 if relu else 0,
-            int(limbs), _lib.ptr(out), _lib.ptr(y_absmax), int(tile_cfg), _lib.stream_ptr()), "smpq_conv2d_fwd")
+        _lib.check(lib.smpq_conv2d_fwd_q(
+            _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, cin, _lib.ptr(codes), int(wlimbs), _lib.ptr(offset), cout,
+            kh, kw, stride, pad, _lib.ptr(col_scale), _lib.ptr(col_shift), _lib.ptr(residual), 1 if relu else 0,
+            int(limbs), _lib.ptr(out), _lib.ptr(y_absmax), _lib.ptr(yq), float(emit_range or 0.0),
+            _lib.ptr(overflow), int(tile_cfg), _lib.stream_ptr()), "smpq_conv2d_fwd_q")
     if hook is not None:
-        hook.end(2 * n * ho * wo * cout * kh * kw * cin, (n, h, w, cin, cout, kh, stride))
+        hook.end(2 * n * ho * wo * cout * kh * kw * min(cin, 3 if cin == 4 else cin), (n, h, w, cin, cout, kh, stride))
+    if emit_range is not None:
+        return out, yq
     return out
 
 
@@ -180,31 +257,38 @@ AUTOTUNE = [os.environ.get("SMPQ_AUTOTUNE", "1") != "0"]
 _TUNED = {}
 
 
-def _tile_fits(cfg, limbs):
+def _tile_fits(cfg, limbs, wlimbs=1, smallc=False):
+    if smallc and cfg not in (2, 3):
+        return False
     bm, bn, nt = tile_configs()[cfg]
     waves = nt // 64
-    return limbs * (bm // 16) * (bn // 16) // waves * 4 <= 128
+    return (limbs + wlimbs - 1) * (bm // 16) * (bn // 16) // waves * 4 <= 128
 
 
 def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
-                   residual=None, relu=False, y_absmax=None, out=None):
+                   residual=None, relu=False, y_absmax=None, out=None, emit_range=None, overflow=None,
+                   want_f32=True):
     """conv2d_q with the fastest tile for this shape (timed once per shape, then cached).
     Every tile gives bitwise-identical results (exact integer accumulation, same epilogue)."""
     limbs, n, h, w, cin = xq.shape
-    key = (n, h, w, cin, codes.shape[0], kh, kw, stride, pad, limbs, residual is not None)
+    wlimbs = codes.shape[0] if codes.dim() == 3 else 1
+    cout = codes.shape[-2]
+    key = (n, h, w, cin, cout, kh, kw, stride, pad, limbs, wlimbs, residual is not None, emit_range is not None,
+           want_f32)
     cfg = _TUNED.get(key)
     if cfg is None and AUTOTUNE[0] and not torch.cuda.is_current_stream_capturing():
         best = None
         for c in tile_configs():
-            if not _tile_fits(c, limbs):
+            if not _tile_fits(c, limbs, wlimbs, cin == 4):
                 continue
             times = []
             for rep in range(3):
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-                out = conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
-                               residual=residual, relu=relu, y_absmax=y_absmax, out=out, tile_cfg=c)
+                conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
+                         residual=residual, relu=relu, y_absmax=y_absmax, out=out, tile_cfg=c,
+                         emit_range=emit_range, overflow=overflow, want_f32=want_f32)
                 e1.record()
                 times.append((e0, e1))
             torch.cuda.synchronize()
@@ -215,7 +299,8 @@ def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, 
         _TUNED[key] = cfg
     return conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
                     residual=residual, relu=relu, y_absmax=y_absmax, out=out,
-                    tile_cfg=-1 if cfg is None else cfg)
+                    tile_cfg=-1 if cfg is None else cfg, emit_range=emit_range, overflow=overflow,
+                    want_f32=want_f32)
 
 
 def conv2d_nhwc(x, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,

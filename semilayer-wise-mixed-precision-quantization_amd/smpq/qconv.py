@@ -12,10 +12,11 @@ weight. The packed int8 codes are rebuilt whenever the weight or the metadata ch
 (smpq_pack_weights): a channel whose weight is not ``fl32(m * step)`` is never run through
 the integer path.
 
-Channels that were never quantized (bit 32 in the reference's bookkeeping, e.g. mid-search
-semilayers) have no integer representation; a conv with any such channel runs the plain fp32
-``F.conv2d`` (MIOpen) — exactly the reference's arithmetic for unquantized weights — and is
-counted in ``smpq.stats``.
+Channels that were never quantized (bit 32 in the reference's bookkeeping: the stem, the
+downsample convs, mid-search semilayers) have no integer code; they run on the same HIP kernel
+with their fp32 weights in per-channel fixed point with as many int8 limbs as the activations
+(16 or 24 bits), counted in ``smpq.stats["fixed_conv"]``. Only geometries the kernel does not cover (groups, dilation,
+cin not in {<=4, 64k}) fall back to ``F.conv2d`` (counted in ``stats["fp32_conv"]``).
 """
 import weakref
 
@@ -26,7 +27,7 @@ import torch.nn.functional as F
 
 from . import ops
 
-stats = {"hip_conv": 0, "fp32_conv": 0, "repack": 0}
+stats = {"hip_conv": 0, "fixed_conv": 0, "fp32_conv": 0, "repack": 0}
 _REGISTRY = weakref.WeakSet()
 
 
@@ -109,26 +110,44 @@ class QConv2d(nn.Conv2d):
     def _pack_key(self):
         w = self.weight
         return (w.data_ptr(), w._version, w.device, self._meta_gen, self.qstep.data_ptr(),
-                self.qstep._version, self.qbits._version)
+                self.qstep._version, self.qbits._version, ops.get_act_limbs())
+
+    def hip_supported(self):
+        return (self.weight.is_cuda and self.groups == 1 and self.dilation == (1, 1)
+                and self.padding_mode == "zeros" and self.stride[0] == self.stride[1]
+                and self.padding[0] == self.padding[1]
+                and (self.in_channels <= 4 or self.in_channels % 64 == 0))
 
     def packed(self):
-        """(codes, offset_or_None) for the HIP kernel, or None if the layer must run in fp32."""
-        if not self.weight.is_cuda or self.groups != 1 or self.dilation != (1, 1) \
-                or self.in_channels % 64 != 0 or self.padding_mode != "zeros" \
-                or not self.fully_quantized():
+        """Weight operand of the HIP conv: (codes int8 [LW, cout, K], LW, offset | None,
+        wscale fp32 [cout], kind), kind one of
+          'exact8'  every channel quantized, exact int8 codes (LW = 1) — the hot path;
+          'exact16' every channel quantized, exact codes needing 2 limbs (e.g. 257-level ties);
+          'fixed'   some channels never quantized (fp32 weights, e.g. the stem, the downsample,
+                    mid-search layers): those channels in per-channel fixed point with as many
+                    int8 limbs as the activations (LW = max(2, L): 16 or 24 bits);
+        or None when the conv's geometry is not supported by the kernel."""
+        if not self.hip_supported():
             return None
         key = self._pack_key()
         if self._pack is not None and self._pack[0] == key:
             return self._pack[1]
+        res = None
+        w = self.weight.detach()
         with torch.no_grad():
-            codes, offset, status = ops.pack_weights(self.weight.detach(), self.qstep)
-            st = status.cpu()
-            has_off = bool((offset != 0).any().item())
+            if self.fully_quantized() and self.in_channels % 64 == 0:
+                codes, offset, wscale, status = ops.pack_weights_ex(w, self.qstep, 1)
+                st = status.cpu()
+                if int(st[0]) == 0 and int(st[1]) == 0:
+                    has_off = bool((offset != 0).any().item())
+                    res = (codes, 1, offset if has_off else None, wscale, "exact8")
+            if res is None:
+                step = self.qstep if (self._bits_host > 0).any() else None
+                lw = max(2, ops.get_act_limbs())
+                codes, _, wscale, status = ops.pack_weights_ex(w, step, lw)
+                kind = "fixed" if int(status.cpu()[2]) > 0 else "exact16"
+                res = (codes, lw, None, wscale, kind)
         stats["repack"] += 1
-        if int(st[0]) or int(st[1]):
-            res = None  # weights not on the recorded grid, or > 256 levels: fp32 path
-        else:
-            res = (codes, offset if has_off else None)
         self._pack = (key, res)
         return res
 
@@ -141,13 +160,22 @@ class QConv2d(nn.Conv2d):
             stats["fp32_conv"] += 1
             self.last_path = "fp32"
             return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
-        codes, offset = pk
+        codes, lw, offset, wscale, kind = pk
         stats["hip_conv"] += 1
-        self.last_path = "hip"
-        xh = x.float().permute(0, 2, 3, 1).contiguous()
-        amax = ops.act_absmax(xh)
+        if kind == "fixed":
+            stats["fixed_conv"] += 1
+        self.last_path = "hip-" + kind
+        x = x.float()
+        if self.in_channels <= 4:
+            xc = x.contiguous()
+            amax = ops.act_absmax(xc)
+            xq = ops.image_quantize(xc, amax)
+        else:
+            xh = x.permute(0, 2, 3, 1).contiguous()
+            amax = ops.act_absmax(xh)
+            xq = ops.act_quantize(xh, amax)
         shift = self.bias.detach().float().contiguous() if self.bias is not None else \
             torch.zeros(self.out_channels, dtype=torch.float32, device=x.device)
-        y = ops.conv2d_nhwc(xh, amax, codes, offset, self.kernel_size[0], self.kernel_size[1],
-                            self.stride[0], self.padding[0], self.qstep.contiguous(), shift)
+        y = ops.tuned_conv2d_q(xq, amax, codes, offset, self.kernel_size[0], self.kernel_size[1],
+                               self.stride[0], self.padding[0], wscale.contiguous(), shift)
         return y.permute(0, 3, 1, 2)

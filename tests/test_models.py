@@ -35,7 +35,7 @@ def test_state_dict_keys_are_torchvision_plus_metadata():
     keys = set(net.state_dict())
     assert "layer1.0.conv1.weight" in keys and "fc.bias" in keys and "layer1.0.downsample.0.weight" in keys
     extra = {k for k in keys if k.endswith(".qbits") or k.endswith(".qstep")}
-    assert len(extra) == 2 * (48 + 4)
+    assert len(extra) == 2 * (48 + 4 + 1)  # addressable + downsample + stem
     # a plain torchvision-style state dict (no metadata) loads strictly
     plain = {k: v for k, v in net.state_dict().items() if k not in extra}
     net2 = resnet.resnet50()
