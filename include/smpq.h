@@ -151,13 +151,16 @@ int smpq_conv2d_fwd_ex(const int8_t* xq, const float* x_absmax, int n, int h, in
  *   yq         int8 [limbs][n*ho*wo][cout] planes of q = clamp(rne(y * QMAX / yq_range)), or NULL
  *   yq_range   static per-layer range (> 0) of the output quantizer (calibrated by the caller)
  *   overflow   device int32 [1]: set to 1 when some |y| > yq_range (values are then clamped; the
- *              caller re-runs with dynamic ranges) */
+ *              caller re-runs with dynamic ranges)
+ *   residual_q int8 [limbs][n*ho*wo][cout] limb planes of the residual (e.g. the block input as
+ *              written by the previous conv's yq), dequantized as residual_range/QMAX * q; NULL
+ *              when `residual` (fp32) or no residual is used */
 int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                       const int8_t* codes, int wlimbs, const int32_t* offset, int cout, int kh,
                       int kw, int stride, int pad, const float* col_scale, const float* col_shift,
                       const float* residual, int relu, int limbs, float* y, float* y_absmax,
-                      int8_t* yq, float yq_range, int32_t* overflow, int tile_cfg,
-                      smpq_stream_t stream);
+                      int8_t* yq, float yq_range, int32_t* overflow, const int8_t* residual_q,
+                      float residual_range, int tile_cfg, smpq_stream_t stream);
 
 /* Tile configurations of smpq_conv2d_fwd (for autotuning): count, and BM x BN / threads. */
 int smpq_conv2d_num_tile_configs(void);

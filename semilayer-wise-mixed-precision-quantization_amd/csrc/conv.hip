@@ -19,9 +19,11 @@
 // Activations: L int8 limbs of a per-image fixed point q = rne(x * QMAX / max|x_img|)
 // (act_quantize_kernel), L = 1 / 2 / 3 -> int8 / int16 / int24.
 // Each (activation limb, weight limb) pair is one MFMA pass; passes of equal total weight
-// 256^(la+lw) share an int32 accumulator; the NACC = L + LW - 1 accumulators are recombined in
-// fp32 in the epilogue. All accumulation is exact integer arithmetic, so results are independent
-// of the tile configuration and of the batch composition (per-image steps).
+// 256^(la+lw) share an int32 accumulator, recombined in fp32 in the epilogue. With 3-limb operands
+// on both sides (24-bit x 24-bit) the passes with la + lw < SMIN = L + LW - 4 (products of two low
+// digits, weight <= 2^-22 of the top product, i.e. below the 24-bit quantization step itself) are
+// skipped: 6 passes instead of 9. All accumulation is exact integer arithmetic, so results are
+// independent of the tile configuration and of the batch composition (per-image steps).
 //
 // Tile: WAVES_M x WAVES_N waves; each wave owns WM x WN subtiles of 16 x 16 computed with
 // v_mfma_i32_16x16x64_i8. Global -> register prefetch of K step k+1 overlaps the MFMAs of step
@@ -45,7 +47,9 @@ struct ConvArgs {
   const int32_t* w_off;  // [cout] (LW == 1 only) or NULL
   const float* col_scale;
   const float* col_shift;
-  const float* residual;
+  const float* residual;   // fp32 NHWC residual, or NULL
+  const int8_t* res_q;     // [L][M][cout] residual limb planes (static range), or NULL
+  float res_scale;         // residual value = res_scale * sum_l 256^l digit_l
   float* y;              // fp32 NHWC output, or NULL
   float* y_absmax;
   int8_t* yq;            // [L][M][cout] output limb planes (static range), or NULL
@@ -80,7 +84,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int BM = 16 * WM * WAVES_M;
   constexpr int BN = 16 * WN * WAVES_N;
-  constexpr int NACC = L + LW - 1;
+  constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;  // lowest accumulated limb weight
+  constexpr int NACC = L + LW - 1 - SMIN;
   constexpr int RPP = NT / 4;                  // 64-B rows covered per pass (4 threads per row)
   constexpr int AR = (BM + RPP - 1) / RPP;     // A rows per thread per limb
   constexpr int BROWS = (BN + RPP - 1) / RPP;  // B rows per thread per limb
@@ -265,11 +270,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
           rs[l][i] = s;
         }
 #pragma unroll
-        for (int lw = 0; lw < LW; ++lw)
+        for (int lw = 0; lw < LW; ++lw) {
+          if (l + lw < SMIN) continue;  // compile-time: skipped low-digit product
 #pragma unroll
           for (int j = 0; j < WN; ++j)
-            acc[l + lw][i][j] =
-                __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[lw][j], acc[l + lw][i][j], 0, 0, 0);
+            acc[l + lw - SMIN][i][j] =
+                __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[lw][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
+        }
       }
     }
 
@@ -308,7 +315,31 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
   constexpr int V4 = BN / 4;  // float4 per tile row
   const bool vec_ok = (a.cout & 3) == 0;
   __syncthreads();
-  if (a.residual) {
+  if (a.res_q) {
+    // residual from the block input's int8 limb planes: 4*L bytes per 4 channels instead of 16
+    const long long rplane = (long long)a.M * a.cout;
+    for (int e = tid; e < BM * V4; e += NT) {
+      const int r = e / V4, c4 = e - (e / V4) * V4;
+      const int m = m0 + r, col = n0 + 4 * c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m < a.M && col < a.cout) {
+        int q[4] = {0, 0, 0, 0};
+        const int8_t* src = a.res_q + (size_t)m * a.cout + col;
+        int limbw = 1;
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+          const unsigned int wd = *reinterpret_cast<const unsigned int*>(src + l * rplane);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) q[k] += (int)(int8_t)(wd >> (8 * k)) * limbw;
+          limbw *= 256;
+        }
+        v = make_float4(a.res_scale * (float)q[0], a.res_scale * (float)q[1], a.res_scale * (float)q[2],
+                        a.res_scale * (float)q[3]);
+      }
+      *reinterpret_cast<float4*>(&tile[r * TS + 4 * c4]) = v;
+    }
+    __syncthreads();
+  } else if (a.residual) {
     for (int e = tid; e < BM * V4; e += NT) {
       const int r = e / V4, c4 = e - (e / V4) * V4;
       const int m = m0 + r, col = n0 + 4 * c4;
@@ -343,17 +374,17 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
       for (int j = 0; j < WN; ++j) {
         const int cloc = bcol_base + 16 * j + frow;
         float v = 0.f;
-        float limbw = 1.f;
+        float limbw = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
 #pragma unroll
         for (int s = 0; s < NACC; ++s) {
           int t = acc[s][i][j][r];
-          if (s < L) t += coloff[j] * rsum[s];
+          if (SMIN == 0 && s < L) t += coloff[j] * rsum[s];  // offsets only exist for LW == 1
           v += (float)t * limbw;
           limbw *= 256.f;
         }
         float out = v * (rscale * colscale[j]) + colshift[j];
         float* tp = &tile[rloc * TS + cloc];
-        if (a.residual) out += *tp;
+        if (a.residual || a.res_q) out += *tp;
         if (a.relu) out = fmaxf(out, 0.f);
         *tp = out;
         if (n0 + cloc < a.cout) rmax = fmaxf(rmax, fabsf(out));
@@ -577,8 +608,14 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x
   } else {
     for (int64_t i = start / 4; i < per_image; i += stride / 4) m = fmaxf(m, fabsf(p[i]));
   }
+  __shared__ float red[4];
   m = wave_max(m);
-  if ((threadIdx.x & 63) == 0 && m > 0.f) atomic_max_nonneg(&out[img], m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (m > 0.f) atomic_max_nonneg(&out[img], m);
+  }
 }
 
 __global__ void debug_mfma_kernel(const int8_t* a, const int8_t* b, int32_t* c) {
@@ -595,7 +632,8 @@ __global__ void debug_mfma_kernel(const int8_t* a, const int8_t* b, int32_t* c) 
 // ------------------------------------------------------------------------------------------
 template <int L, int LW, bool SMALLC, int WAVES_M, int WAVES_N, int WM, int WN, int MINW>
 static int launch(const ConvArgs& a, hipStream_t stream) {
-  if constexpr ((L + LW - 1) * WM * WN * 4 > 128) {
+  constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
+  if constexpr ((L + LW - 1 - SMIN) * WM * WN * 4 > 128) {
     // more than 128 accumulator registers per lane: not instantiated (would spill)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: tile config too large for these limb counts");
   } else {
@@ -650,7 +688,7 @@ static int launch_cfg(int cfg, bool smallc, const ConvArgs& a, hipStream_t s) {
 
 // Default tile when the caller does not pass one (the Python layer autotunes per shape).
 static int heuristic_cfg(int nacc, long M, int cout, int K, bool smallc) {
-  if (nacc >= 4) return 3;
+  if (nacc >= 4) return 3;  // (accumulator sets after skipping; see SMIN)
   if (smallc) return 2;
   if (cout <= 64) return M >= 128L * 512 ? 2 : 3;
   if (nacc >= 3) return 3;
@@ -667,12 +705,15 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
                                  int kw, int stride, int pad, const float* col_scale,
                                  const float* col_shift, const float* residual, int relu, int limbs,
                                  float* y, float* y_absmax, int8_t* yq, float yq_range, int32_t* overflow,
-                                 int tile_cfg, smpq_stream_t stream) {
+                                 const int8_t* residual_q, float residual_range, int tile_cfg,
+                                 smpq_stream_t stream) {
   if (!xq || !x_absmax || !codes || !col_scale || !col_shift || (!y && !yq))
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: null pointer");
   if (yq && (!overflow || !(yq_range > 0.f)))
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: yq needs overflow flag and a positive range");
-  if (yq && (cout & 3) != 0) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: yq needs cout % 4 == 0");
+  if ((yq || residual_q) && (cout & 3) != 0)
+    return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: limb-plane output/residual needs cout % 4 == 0");
+  if (residual_q && residual) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: two residuals");
   if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || stride <= 0 ||
       pad < 0)
     return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: bad shape");
@@ -692,6 +733,8 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
   a.col_scale = col_scale;
   a.col_shift = col_shift;
   a.residual = residual;
+  a.res_q = residual_q;
+  a.res_scale = residual_q ? residual_range / (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f)) : 0.f;
   a.y = y;
   a.y_absmax = y_absmax;
   a.yq = yq;
@@ -727,7 +770,10 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
   a.relu = relu ? 1 : 0;
   a.has_offset = (offset && wlimbs == 1) ? 1 : 0;
   hipStream_t s = (hipStream_t)stream;
-  if (tile_cfg < 0) tile_cfg = heuristic_cfg(limbs + wlimbs - 1, M, cout, a.K, smallc);
+  if (tile_cfg < 0) {
+    const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
+    tile_cfg = heuristic_cfg(limbs + wlimbs - 1 - smin, M, cout, a.K, smallc);
+  }
   if (tile_cfg >= kNumTileCfgs) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   if (limbs < 1 || limbs > 3) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: limbs must be 1, 2 or 3");
   a.inv_qmax = 1.f / (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f));
@@ -754,7 +800,7 @@ extern "C" int smpq_conv2d_fwd_ex(const int8_t* xq, const float* x_absmax, int n
   if (!y) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: null pointer");
   return smpq_conv2d_fwd_q(xq, x_absmax, n, h, w, cin, codes, wlimbs, offset, cout, kh, kw, stride, pad,
                            col_scale, col_shift, residual, relu, limbs, y, y_absmax, nullptr, 0.f, nullptr,
-                           tile_cfg, stream);
+                           nullptr, 0.f, tile_cfg, stream);
 }
 
 extern "C" int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
@@ -844,8 +890,10 @@ extern "C" int smpq_act_absmax(const float* x, int n, int64_t per_image, float* 
                                smpq_stream_t stream) {
   if (!x || !absmax || n <= 0 || per_image <= 0)
     return fail(SMPQ_E_INVALID, "smpq_act_absmax: bad arguments");
-  int chunks = (int)((per_image / 4 + 255) / 256);
-  if (chunks > 64) chunks = 64;
+  // ~2 workgroups per CU in total, few atomics per image (no contention on one address)
+  int chunks = (512 + n - 1) / n;
+  const int maxc = (int)((per_image / 4 + 255) / 256);
+  if (chunks > maxc) chunks = maxc;
   if (chunks < 1) chunks = 1;
   hipLaunchKernelGGL(absmax_kernel, dim3(chunks, n), dim3(256), 0, (hipStream_t)stream, x, per_image,
                      absmax);

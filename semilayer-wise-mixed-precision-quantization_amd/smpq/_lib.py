@@ -48,7 +48,7 @@ _PROTOS = {
     "smpq_conv2d_fwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp,
                              _vp, _i, _i, _vp, _vp, _i, _vp]),
     "smpq_conv2d_fwd_q": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp,
-                               _vp, _i, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _i, _vp]),
+                               _vp, _i, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, ctypes.c_float, _i, _vp]),
     "smpq_conv2d_num_tile_configs": (_i, []),
     "smpq_conv2d_tile_config": (_i, [_i, _vp, _vp, _vp]),
     "smpq_conv2d_workspace_bytes": (ctypes.c_size_t, [_i] * 10),

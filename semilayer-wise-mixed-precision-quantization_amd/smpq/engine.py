@@ -50,10 +50,10 @@ def get_range_mode():
 
 
 class Act:
-    __slots__ = ("f32", "q", "amax")
+    __slots__ = ("f32", "q", "amax", "rng")
 
-    def __init__(self, f32=None, q=None, amax=None):
-        self.f32, self.q, self.amax = f32, q, amax
+    def __init__(self, f32=None, q=None, amax=None, rng=None):
+        self.f32, self.q, self.amax, self.rng = f32, q, amax, rng  # rng: static range (float) or None
 
     def limbs(self):
         if self.q is None:
@@ -113,23 +113,31 @@ def _to_nhwc(x):
 class Ctx:
     """Per-forward state: range mode, calibrated ranges, recorded maxima, overflow flag."""
 
-    def __init__(self, n, device, ranges=None, record=False):
+    def __init__(self, n, device, ranges=None, record=False, cache=None):
         self.n, self.device = n, device
         self.ranges = ranges            # {id(conv): range} (static mode) or None
         self.record = {} if record else None
         self.overflow = torch.zeros(1, dtype=torch.int32, device=device) if ranges else None
-        self._rt = {}
+        self._rt = cache if cache is not None else {}
 
     def range_tensor(self, conv):
-        t = self._rt.get(id(conv))
+        key = (id(conv), self.n)
+        t = self._rt.get(key)
         if t is None:
             t = torch.full((self.n,), self.ranges[id(conv)], dtype=torch.float32, device=self.device)
-            self._rt[id(conv)] = t
+            self._rt[key] = t
         return t
 
 
 def run_conv(conv, bn, act, relu, residual=None, want_amax=True, ctx=None, want_f32=True):
-    """y = act(bn(conv(x)) [+ residual]) -> Act (NHWC fp32 and/or the next conv's limb planes)."""
+    """y = act(bn(conv(x)) [+ residual]) -> Act (NHWC fp32 and/or the next conv's limb planes).
+    ``residual``: an fp32 NHWC tensor, or an Act carrying limb planes + static range."""
+    res_q = res_rng = None
+    if isinstance(residual, Act):
+        if residual.f32 is not None:
+            residual = residual.f32
+        else:
+            res_q, res_rng, residual = residual.q, residual.rng, None
     n = act.amax.shape[0] if act.amax is not None else act.f32.shape[0]
     plan = conv_plan(conv, bn)
     static = ctx is not None and ctx.ranges is not None and want_amax and plan is not None \
@@ -146,11 +154,12 @@ def run_conv(conv, bn, act, relu, residual=None, want_amax=True, ctx=None, want_
             y, yq = ops.tuned_conv2d_q(act.limbs(), act.amax, codes, offset, conv.kernel_size[0],
                                        conv.kernel_size[1], conv.stride[0], conv.padding[0], col_scale, col_shift,
                                        residual=residual, relu=relu, emit_range=rng, overflow=ctx.overflow,
-                                       want_f32=want_f32)
-            return Act(f32=y, q=yq, amax=ctx.range_tensor(conv))
+                                       want_f32=want_f32, residual_q=res_q, residual_range=res_rng)
+            return Act(f32=y, q=yq, amax=ctx.range_tensor(conv), rng=rng)
         y = ops.tuned_conv2d_q(act.limbs(), act.amax, codes, offset, conv.kernel_size[0], conv.kernel_size[1],
                                conv.stride[0], conv.padding[0], col_scale, col_shift,
-                               residual=residual, relu=relu, y_absmax=yam)
+                               residual=residual, relu=relu, y_absmax=yam, residual_q=res_q,
+                               residual_range=res_rng)
         if ctx is not None and ctx.record is not None and yam is not None:
             ctx.record[id(conv)] = yam
         return Act(f32=y, amax=yam)
@@ -163,6 +172,8 @@ def run_conv(conv, bn, act, relu, residual=None, want_amax=True, ctx=None, want_
         y = F.batch_norm(y, bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
     if residual is not None:
         y = y + _to_nchw(residual)
+    elif res_q is not None:
+        raise RuntimeError("smpq: limb-plane residual on the fp32 fallback path")
     if relu:
         y = F.relu(y)
     y = _to_nhwc(y)
@@ -172,20 +183,25 @@ def run_conv(conv, bn, act, relu, residual=None, want_amax=True, ctx=None, want_
 
 
 def block_forward(blk, x, ctx=None, last=False):
-    """One BasicBlock / Bottleneck on an Act; returns the output Act. Block-internal activations
-    never need fp32 in static mode; the block output keeps fp32 (identity path, avgpool)."""
+    """One BasicBlock / Bottleneck on an Act; returns the output Act. In static mode no
+    activation is stored in fp32 except the downsample's identity and the last block's output
+    (avgpool): the identity of a block without downsample is read from its input's limb planes."""
     if blk.downsample is not None:
         identity = run_conv(blk.downsample[0], blk.downsample[1], x, relu=False, want_amax=False, ctx=ctx).f32
-    else:
+    elif x.f32 is not None or x.q is None or x.rng is None:
         identity = x.f32
+    else:
+        identity = x
     out_amax = not last  # the last block feeds only avgpool
     if hasattr(blk, "conv3"):  # Bottleneck (resnet.py:97-116)
         t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
         t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
-        return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax)
+        return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax,
+                        want_f32=last)
     # BasicBlock (resnet.py:55-68)
     t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
-    return run_conv(blk.conv2, blk.bn2, t1, True, residual=identity, ctx=ctx, want_amax=out_amax)
+    return run_conv(blk.conv2, blk.bn2, t1, True, residual=identity, ctx=ctx, want_amax=out_amax,
+                    want_f32=last)
 
 
 def stem_forward(model, x):
@@ -244,7 +260,7 @@ def calibrate(model, x):
             if old is not None and old[1] == _signature(model) and k in old[0]:
                 r = max(r, old[0][k])
             ranges[k] = r
-        model._smpq_ranges = (ranges, _signature(model))
+        model._smpq_ranges = (ranges, _signature(model), {})
     stats["calibrations"] += 1
     return y
 
@@ -256,7 +272,7 @@ def forward_fused(model, x):
     cal = getattr(model, "_smpq_ranges", None)
     if cal is None or cal[1] != _signature(model):
         return calibrate(model, x)
-    ctx = Ctx(x.shape[0], x.device, ranges=cal[0])
+    ctx = Ctx(x.shape[0], x.device, ranges=cal[0], cache=cal[2])
     y = _forward(model, x, ctx)
     if int(ctx.overflow.item()) == 0:  # one sync: results are never silently clamped
         return y

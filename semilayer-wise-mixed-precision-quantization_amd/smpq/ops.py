@@ -194,13 +194,14 @@ def tile_configs():
 
 def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
              residual=None, relu=False, y_absmax=None, out=None, tile_cfg=-1,
-             emit_range=None, overflow=None, want_f32=True):
+             emit_range=None, overflow=None, want_f32=True, residual_q=None, residual_range=None):
     """Quantized conv on int8 limb planes xq [L, n, h, w, cin] (from act_quantize / image_quantize /
     maxpool_quantize / a previous conv2d_q) and weight limb planes codes [LW, cout, K] (or
     [cout, K] for LW = 1): y = conv(x, w) * s_x * col_scale + col_shift (+res) (relu), NHWC fp32.
     With ``emit_range`` (static range of the output, float) the epilogue also writes the output's
     int8 limb planes [L, n, ho, wo, cout] and sets ``overflow`` (int32 [1]) if a value exceeded the
-    range; returns (y or None, yq) then."""
+    range; returns (y or None, yq) then. ``residual_q`` (+ ``residual_range``): the residual as
+    int8 limb planes [L, n, ho, wo, cout] instead of fp32 ``residual``."""
     _req(xq.is_cuda and xq.dtype == torch.int8 and xq.dim() == 5 and xq.is_contiguous(), "conv: xq must be [L,n,h,w,c] int8")
     limbs, n, h, w, cin = xq.shape
     _req(limbs in (1, 2, 3), "conv: limbs")
@@ -233,6 +234,10 @@ def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_sh
     if residual is not None:
         _req(residual.shape == (n, ho, wo, cout) and residual.is_contiguous() and residual.dtype == torch.float32,
              "conv: residual shape")
+    if residual_q is not None:
+        _req(residual is None and residual_q.shape == (limbs, n, ho, wo, cout) and residual_q.dtype == torch.int8
+             and residual_q.is_contiguous() and residual_range is not None and residual_range > 0
+             and cout % 4 == 0, "conv: residual_q")
     if y_absmax is not None:
         _req(y_absmax.numel() == n and y_absmax.dtype == torch.float32, "conv: y_absmax")
     lib = _lib.load()
@@ -244,7 +249,8 @@ def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_sh
             _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, cin, _lib.ptr(codes), int(wlimbs), _lib.ptr(offset), cout,
             kh, kw, stride, pad, _lib.ptr(col_scale), _lib.ptr(col_shift), _lib.ptr(residual), 1 if relu else 0,
             int(limbs), _lib.ptr(out), _lib.ptr(y_absmax), _lib.ptr(yq), float(emit_range or 0.0),
-            _lib.ptr(overflow), int(tile_cfg), _lib.stream_ptr()), "smpq_conv2d_fwd_q")
+            _lib.ptr(overflow), _lib.ptr(residual_q), float(residual_range or 0.0), int(tile_cfg),
+            _lib.stream_ptr()), "smpq_conv2d_fwd_q")
     if hook is not None:
         hook.end(2 * n * ho * wo * cout * kh * kw * min(cin, 3 if cin == 4 else cin), (n, h, w, cin, cout, kh, stride))
     if emit_range is not None:
@@ -262,19 +268,20 @@ def _tile_fits(cfg, limbs, wlimbs=1, smallc=False):
         return False
     bm, bn, nt = tile_configs()[cfg]
     waves = nt // 64
-    return (limbs + wlimbs - 1) * (bm // 16) * (bn // 16) // waves * 4 <= 128
+    smin = max(0, limbs + wlimbs - 4)  # low-digit passes skipped by the kernel (see conv.hip)
+    return (limbs + wlimbs - 1 - smin) * (bm // 16) * (bn // 16) // waves * 4 <= 128
 
 
 def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
                    residual=None, relu=False, y_absmax=None, out=None, emit_range=None, overflow=None,
-                   want_f32=True):
+                   want_f32=True, residual_q=None, residual_range=None):
     """conv2d_q with the fastest tile for this shape (timed once per shape, then cached).
     Every tile gives bitwise-identical results (exact integer accumulation, same epilogue)."""
     limbs, n, h, w, cin = xq.shape
     wlimbs = codes.shape[0] if codes.dim() == 3 else 1
     cout = codes.shape[-2]
     key = (n, h, w, cin, cout, kh, kw, stride, pad, limbs, wlimbs, residual is not None, emit_range is not None,
-           want_f32)
+           want_f32, residual_q is not None)
     cfg = _TUNED.get(key)
     if cfg is None and AUTOTUNE[0] and not torch.cuda.is_current_stream_capturing():
         best = None
@@ -288,7 +295,8 @@ def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, 
                 e0.record()
                 conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
                          residual=residual, relu=relu, y_absmax=y_absmax, out=out, tile_cfg=c,
-                         emit_range=emit_range, overflow=overflow, want_f32=want_f32)
+                         emit_range=emit_range, overflow=overflow, want_f32=want_f32,
+                         residual_q=residual_q, residual_range=residual_range)
                 e1.record()
                 times.append((e0, e1))
             torch.cuda.synchronize()
@@ -300,7 +308,7 @@ def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, 
     return conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
                     residual=residual, relu=relu, y_absmax=y_absmax, out=out,
                     tile_cfg=-1 if cfg is None else cfg, emit_range=emit_range, overflow=overflow,
-                    want_f32=want_f32)
+                    want_f32=want_f32, residual_q=residual_q, residual_range=residual_range)
 
 
 def conv2d_nhwc(x, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,

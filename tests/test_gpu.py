@@ -392,9 +392,12 @@ def emulate_limbs(xq_planes, wq_planes, k, stride, pad, rscale, col_scale, col_s
     n = xq_planes.shape[1]
     v = 0.0
     mag = 0.0
+    smin = max(0, xq_planes.shape[0] + wq_planes.shape[0] - 4)  # kernel skips la + lw < smin
     for la in range(xq_planes.shape[0]):
         cols, ho, wo = im2col_nhwc(xq_planes[la].astype(np.float64), k, stride, pad)
         for lw in range(wq_planes.shape[0]):
+            if la + lw < smin:
+                continue
             t = cols @ wq_planes[lw].reshape(wq_planes.shape[1], -1).T.astype(np.float64) * 256.0 ** (la + lw)
             v = v + t
             mag = mag + np.abs(t)
