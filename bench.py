@@ -106,6 +106,7 @@ def main():
     ap.add_argument("--limbs", type=int, default=2, help="activation int8 limbs (2 = int16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--chunk", type=int, default=None, help="images per pass (Infinity-Cache blocking)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,6 +128,9 @@ def main():
 
     arch, assign, desc = CONFIGS[args.config]
     ops.set_act_limbs(args.limbs)
+    from smpq import engine
+    if args.chunk:
+        engine.set_chunk(args.chunk)
     torch.manual_seed(0)
     net = getattr(resnet, arch)().to(dev).eval()
     assignments.apply_assignment(net, assign)
@@ -194,7 +198,8 @@ def main():
             "config": {"workload": desc, "assignment": assign, "batch_per_gpu": args.batch,
                        "global_batch": args.batch * world, "act_limbs": args.limbs,
                        "act_code": {1: "int8", 2: "int16 (2 int8 limbs)", 3: "int24 (3 int8 limbs)"}[args.limbs],
-                       "parallelism": "dp%d" % world, "quantized_convs_per_step": hip_convs // max(args.steps, 1)},
+                       "parallelism": "dp%d" % world, "quantized_convs_per_step": hip_convs // max(args.steps, 1),
+                       "range_mode": engine.get_range_mode(), "chunk": engine.CHUNK[0]},
             "roofline": {"bound": "mfma", "kernel": "qconv_kernel", "achieved": round(achieved_tops, 2),
                          "peak": INT8_DENSE_PEAK_TOPS, "unit": "TFLOP/s",
                          "frac": round(achieved_tops / INT8_DENSE_PEAK_TOPS, 4), "traffic": None,

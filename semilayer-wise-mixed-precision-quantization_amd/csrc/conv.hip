@@ -29,6 +29,7 @@
 // v_mfma_i32_16x16x64_i8. Global -> register prefetch of K step k+1 overlaps the MFMAs of step
 // k; one LDS double buffer, one barrier per K step; the epilogue reuses the LDS arena as an fp32
 // output tile so residual loads and output stores are whole 16-B pieces of contiguous rows.
+#include <cstdlib>
 #include <string>
 
 #include "common.h"
@@ -59,6 +60,8 @@ struct ConvArgs {
   int M, K, ksteps, cchunks;
   int relu, has_offset;
   float inv_qmax;
+  int ablate;  // diagnostics only (SMPQ_ABLATE): 1 no operand loads, 2 no MFMA, 4 no output stores,
+               // 8 no residual loads. Results are wrong with any bit set; never set in production.
 };
 
 template <int L>
@@ -79,7 +82,7 @@ __device__ __host__ constexpr float act_qmax() {
 }
 
 // Block = WAVES_M x WAVES_N waves; each wave owns WM x WN 16x16 subtiles.
-template <int L, int LW, bool SMALLC, int WAVES_M, int WAVES_N, int WM, int WN, int MINW>
+template <int L, int LW, bool SMALLC, int WAVES_M, int WAVES_N, int WM, int WN, int MINW, int PF>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(ConvArgs a) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int BM = 16 * WM * WAVES_M;
@@ -152,10 +155,21 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
     }
   }
 
-  v4i ra[L][AR];
-  v4i rb[LW][BROWS];
+  typedef v4i ASet[L][AR];
+  typedef v4i BSet[LW][BROWS];
 
-  auto load_global = [&](int ks) {
+  auto load_global = [&](int ks, ASet& ra, BSet& rb) {
+    if (a.ablate & 1) {
+#pragma unroll
+      for (int l = 0; l < L; ++l)
+#pragma unroll
+        for (int i = 0; i < AR; ++i) ra[l][i] = v4i{ks, 0, 0, 0};
+#pragma unroll
+      for (int lw = 0; lw < LW; ++lw)
+#pragma unroll
+        for (int j = 0; j < BROWS; ++j) rb[lw][j] = v4i{ks, 1, 0, 0};
+      return;
+    }
     if constexpr (SMALLC) {
       // 16 taps x 4 channels per K step; this thread's piece = taps 16*ks + 4*piece + 0..3
       const int taps = a.kh * a.kw;
@@ -210,7 +224,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
     }
   };
 
-  auto store_lds = [&](int buf) {
+  auto store_lds = [&](int buf, const ASet& ra, const BSet& rb) {
 #pragma unroll
     for (int l = 0; l < L; ++l)
 #pragma unroll
@@ -236,20 +250,14 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
 #pragma unroll
     for (int i = 0; i < WM; ++i) rs[l][i] = 0;
 
-  load_global(0);
-  store_lds(0);
-  __syncthreads();
-
   const int frow = lane & 15;       // fragment row/col owned by this lane
   const int fk = 16 * (lane >> 4);  // fragment K byte offset owned by this lane
   const int arow_base = wm * 16 * WM;
   const int bcol_base = wn * 16 * WN;
   const bool do_off = (LW == 1) && a.has_offset;
 
-  for (int ks = 0; ks < a.ksteps; ++ks) {
-    const int buf = ks & 1;
-    if (ks + 1 < a.ksteps) load_global(ks + 1);
-
+  auto compute = [&](int buf) {
+    if (a.ablate & 2) return;
     v4i bf[LW][WN];
 #pragma unroll
     for (int lw = 0; lw < LW; ++lw)
@@ -279,9 +287,45 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
         }
       }
     }
+  };
 
-    if (ks + 1 < a.ksteps) store_lds(buf ^ 1);
+  if constexpr (PF == 2) {
+  // K loop: two register staging sets, global loads issued two K steps ahead of their use
+  // (latency spans two MFMA phases), one LDS double buffer, one barrier per K step. Unrolled by
+  // two so every register set is statically indexed (no scratch).
+  ASet raA, raB;
+  BSet rbA, rbB;
+  load_global(0, raA, rbA);
+  store_lds(0, raA, rbA);
+  if (a.ksteps > 1) load_global(1, raB, rbB);
+  __syncthreads();
+  int ks = 0;
+  for (; ks + 1 < a.ksteps; ks += 2) {
+    if (ks + 2 < a.ksteps) load_global(ks + 2, raA, rbA);
+    compute(0);
+    store_lds(1, raB, rbB);
     __syncthreads();
+    if (ks + 3 < a.ksteps) load_global(ks + 3, raB, rbB);
+    compute(1);
+    if (ks + 2 < a.ksteps) store_lds(0, raA, rbA);
+    __syncthreads();
+  }
+  if (ks < a.ksteps) compute(0);
+  } else {
+  // K loop: one register staging set, loads issued one K step ahead (fewer live registers:
+  // wins for the tiles with the most accumulators per wave)
+  ASet ra;
+  BSet rb;
+  load_global(0, ra, rb);
+  store_lds(0, ra, rb);
+  __syncthreads();
+  for (int ks = 0; ks < a.ksteps; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < a.ksteps) load_global(ks + 1, ra, rb);
+    compute(buf);
+    if (ks + 1 < a.ksteps) store_lds(buf ^ 1, ra, rb);
+    __syncthreads();
+  }
   }
 
   // ---- epilogue: recombine limbs, affine (dequant * BN), residual, ReLU, store, absmax ----
@@ -315,31 +359,68 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
   constexpr int V4 = BN / 4;  // float4 per tile row
   const bool vec_ok = (a.cout & 3) == 0;
   __syncthreads();
-  if (a.res_q) {
-    // residual from the block input's int8 limb planes: 4*L bytes per 4 channels instead of 16
+  if (a.res_q && !(a.ablate & 8)) {
+    // residual from the block input's int8 limb planes, 16 channels (16 B per limb) per item;
+    // every load of this thread is issued before the first use (constant trip count, unrolled)
+    constexpr int V16 = BN / 16;
+    constexpr int NIT = (BM * V16 + NT - 1) / NT;
     const long long rplane = (long long)a.M * a.cout;
-    for (int e = tid; e < BM * V4; e += NT) {
-      const int r = e / V4, c4 = e - (e / V4) * V4;
-      const int m = m0 + r, col = n0 + 4 * c4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (m < a.M && col < a.cout) {
-        int q[4] = {0, 0, 0, 0};
-        const int8_t* src = a.res_q + (size_t)m * a.cout + col;
-        int limbw = 1;
+    v4i rq[NIT][L];
 #pragma unroll
-        for (int l = 0; l < L; ++l) {
-          const unsigned int wd = *reinterpret_cast<const unsigned int*>(src + l * rplane);
+    for (int it = 0; it < NIT; ++it) {
+      const int e = tid + it * NT;
+      const int r = e / V16, c16 = e - (e / V16) * V16;
+      const int m = m0 + r, col = n0 + 16 * c16;
+      const bool ok = e < BM * V16 && m < a.M && col + 15 < a.cout;
+      const int8_t* src = a.res_q + (size_t)(ok ? m : 0) * a.cout + (ok ? col : 0);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) q[k] += (int)(int8_t)(wd >> (8 * k)) * limbw;
-          limbw *= 256;
-        }
-        v = make_float4(a.res_scale * (float)q[0], a.res_scale * (float)q[1], a.res_scale * (float)q[2],
-                        a.res_scale * (float)q[3]);
+      for (int l = 0; l < L; ++l) {
+        v4i v = {0, 0, 0, 0};
+        if (ok) v = *reinterpret_cast<const v4i*>(src + l * rplane);
+        rq[it][l] = v;
       }
-      *reinterpret_cast<float4*>(&tile[r * TS + 4 * c4]) = v;
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int e = tid + it * NT;
+      if (e >= BM * V16) break;
+      const int r = e / V16, c16 = e - (e / V16) * V16;
+      const int m = m0 + r, col = n0 + 16 * c16;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {  // 4 channels per dword
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < a.M && col + 15 < a.cout) {
+          int q[4] = {0, 0, 0, 0};
+          int limbw = 1;
+#pragma unroll
+          for (int l = 0; l < L; ++l) {
+            const unsigned int wd = (unsigned int)rq[it][l][g];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] += (int)(int8_t)(wd >> (8 * k)) * limbw;
+            limbw *= 256;
+          }
+          v = make_float4(a.res_scale * (float)q[0], a.res_scale * (float)q[1], a.res_scale * (float)q[2],
+                          a.res_scale * (float)q[3]);
+        } else if (m < a.M) {  // ragged channel tail (cout % 16 != 0): bytewise
+          const int8_t* src = a.res_q + (size_t)m * a.cout;
+          float t[4] = {0.f, 0.f, 0.f, 0.f};
+          for (int k = 0; k < 4; ++k) {
+            const int c = col + 4 * g + k;
+            if (c >= a.cout) break;
+            int q = 0, limbw = 1;
+            for (int l = 0; l < L; ++l) {
+              q += (int)src[l * rplane + c] * limbw;
+              limbw *= 256;
+            }
+            t[k] = a.res_scale * (float)q;
+          }
+          v = make_float4(t[0], t[1], t[2], t[3]);
+        }
+        *reinterpret_cast<float4*>(&tile[r * TS + 16 * c16 + 4 * g]) = v;
+      }
     }
     __syncthreads();
-  } else if (a.residual) {
+  } else if (a.residual && !(a.ablate & 8)) {
     for (int e = tid; e < BM * V4; e += NT) {
       const int r = e / V4, c4 = e - (e / V4) * V4;
       const int m = m0 + r, col = n0 + 4 * c4;
@@ -401,12 +482,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
   }
   __syncthreads();
   bool ovf = false;
-  for (int e = tid; e < BM * V4; e += NT) {
-    const int r = e / V4, c4 = e - (e / V4) * V4;
-    const int m = m0 + r, col = n0 + 4 * c4;
-    if (m >= a.M || col >= a.cout) continue;
-    const float4 v = *reinterpret_cast<const float4*>(&tile[r * TS + 4 * c4]);
-    if (a.y) {
+  if (a.y && !(a.ablate & 4)) {
+    for (int e = tid; e < BM * V4; e += NT) {
+      const int r = e / V4, c4 = e - (e / V4) * V4;
+      const int m = m0 + r, col = n0 + 4 * c4;
+      if (m >= a.M || col >= a.cout) continue;
+      const float4 v = *reinterpret_cast<const float4*>(&tile[r * TS + 4 * c4]);
       float* dst = a.y + (size_t)m * a.cout + col;
       if (vec_ok && col + 3 < a.cout) {
         *reinterpret_cast<float4*>(dst) = v;
@@ -417,32 +498,45 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
         if (col + 3 < a.cout) dst[3] = v.w;
       }
     }
-    if (a.yq) {
-      // fused activation quantizer of the NEXT conv's input (static per-layer range)
-      constexpr float qmax = act_qmax<L>();
-      const float vals[4] = {v.x, v.y, v.z, v.w};
-      unsigned int word[L];
+  }
+  if (a.yq && !(a.ablate & 4)) {
+    // fused activation quantizer of the NEXT conv's input (static per-layer range):
+    // 16 channels per item -> one 16-B store per limb plane
+    constexpr float qmax = act_qmax<L>();
+    constexpr int V16 = BN / 16;
+    const long long yplane = (long long)a.M * a.cout;
+    for (int e = tid; e < BM * V16; e += NT) {
+      const int r = e / V16, c16 = e - (e / V16) * V16;
+      const int m = m0 + r, col = n0 + 16 * c16;
+      if (m >= a.M || col >= a.cout) continue;
+      unsigned int word[L][4];
 #pragma unroll
-      for (int l = 0; l < L; ++l) word[l] = 0u;
+      for (int g = 0; g < 4; ++g) {
+        const float4 v = *reinterpret_cast<const float4*>(&tile[r * TS + 16 * c16 + 4 * g]);
+        const float vals[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float qf = rintf(vals[k] * a.yq_inv);
-        ovf |= fabsf(qf) > qmax;
-        qf = fminf(fmaxf(qf, -qmax), qmax);
-        int d[L];
-        split_limbs<L>((int)qf, d);
+        for (int l = 0; l < L; ++l) word[l][g] = 0u;
 #pragma unroll
-        for (int l = 0; l < L; ++l) word[l] |= (unsigned int)(d[l] & 255) << (8 * k);
+        for (int k = 0; k < 4; ++k) {
+          float qf = rintf(vals[k] * a.yq_inv);
+          ovf |= (col + 4 * g + k < a.cout) && fabsf(qf) > qmax;
+          qf = fminf(fmaxf(qf, -qmax), qmax);
+          int d[L];
+          split_limbs<L>((int)qf, d);
+#pragma unroll
+          for (int l = 0; l < L; ++l) word[l][g] |= (unsigned int)(d[l] & 255) << (8 * k);
+        }
       }
       int8_t* dq = a.yq + (size_t)m * a.cout + col;
-      const long long yplane = (long long)a.M * a.cout;
-      if (vec_ok && col + 3 < a.cout) {
-#pragma unroll
-        for (int l = 0; l < L; ++l) *reinterpret_cast<unsigned int*>(dq + l * yplane) = word[l];
-      } else {
+      if (col + 15 < a.cout) {
 #pragma unroll
         for (int l = 0; l < L; ++l)
-          for (int k = 0; k < 4 && col + k < a.cout; ++k) dq[l * yplane + k] = (int8_t)(word[l] >> (8 * k));
+          *reinterpret_cast<v4i*>(dq + l * yplane) =
+              v4i{(int)word[l][0], (int)word[l][1], (int)word[l][2], (int)word[l][3]};
+      } else {
+        for (int l = 0; l < L; ++l)
+          for (int k = 0; k < 16 && col + k < a.cout; ++k)
+            dq[l * yplane + k] = (int8_t)(word[l][k >> 2] >> (8 * (k & 3)));
       }
     }
   }
@@ -630,7 +724,7 @@ __global__ void debug_mfma_kernel(const int8_t* a, const int8_t* b, int32_t* c) 
 }
 
 // ------------------------------------------------------------------------------------------
-template <int L, int LW, bool SMALLC, int WAVES_M, int WAVES_N, int WM, int WN, int MINW>
+template <int L, int LW, bool SMALLC, int WAVES_M, int WAVES_N, int WM, int WN, int MINW, int PF>
 static int launch(const ConvArgs& a, hipStream_t stream) {
   constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
   if constexpr ((L + LW - 1 - SMIN) * WM * WN * 4 > 128) {
@@ -642,7 +736,7 @@ static int launch(const ConvArgs& a, hipStream_t stream) {
     const long nt = (a.cout + BN - 1) / BN;
     const long blocks = mt * nt;
     if (blocks > 0x7fffffffL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
-    hipLaunchKernelGGL((qconv_kernel<L, LW, SMALLC, WAVES_M, WAVES_N, WM, WN, MINW>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((qconv_kernel<L, LW, SMALLC, WAVES_M, WAVES_N, WM, WN, MINW, PF>), dim3((unsigned)blocks),
                        dim3(64 * WAVES_M * WAVES_N), 0, stream, a);
     return check_hip(hipGetLastError(), "qconv_kernel launch");
   }
@@ -660,15 +754,18 @@ constexpr TileCfg kTileCfgs[] = {
     {2, 4, 4, 2},  // 4: 128 x 128, 512 threads (waves 64 x 32)
     {4, 2, 2, 4},  // 5: 128 x 128, 512 threads (waves 32 x 64)
 };
-constexpr int kNumTileCfgs = sizeof(kTileCfgs) / sizeof(kTileCfgs[0]);
+constexpr int kNumBaseCfgs = sizeof(kTileCfgs) / sizeof(kTileCfgs[0]);
+// Configs [0, 6) stage global loads two K steps ahead, [6, 12) are the same tiles with one step
+// of prefetch (fewer live registers). Neither wins everywhere; the host autotuner picks.
+constexpr int kNumTileCfgs = 2 * kNumBaseCfgs;
 
-template <int L, int LW>
+template <int L, int LW, int PF>
 static int launch_cfg(int cfg, bool smallc, const ConvArgs& a, hipStream_t s) {
   if (smallc) {
     if constexpr (LW >= 2 && L >= 2) {
       switch (cfg) {
-        case 2: return launch<L, LW, true, 2, 2, 4, 2, 2>(a, s);
-        case 3: return launch<L, LW, true, 2, 2, 2, 2, 4>(a, s);
+        case 2: return launch<L, LW, true, 2, 2, 4, 2, 2, PF>(a, s);
+        case 3: return launch<L, LW, true, 2, 2, 2, 2, 4, PF>(a, s);
         default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: cin==4 supports tile configs 2, 3");
       }
     } else {
@@ -676,13 +773,30 @@ static int launch_cfg(int cfg, bool smallc, const ConvArgs& a, hipStream_t s) {
     }
   }
   switch (cfg) {
-    case 0: return launch<L, LW, false, 2, 2, 4, 4, 2>(a, s);
-    case 1: return launch<L, LW, false, 2, 2, 2, 4, 2>(a, s);
-    case 2: return launch<L, LW, false, 2, 2, 4, 2, 2>(a, s);
-    case 3: return launch<L, LW, false, 2, 2, 2, 2, 4>(a, s);
-    case 4: return launch<L, LW, false, 2, 4, 4, 2, 2>(a, s);
-    case 5: return launch<L, LW, false, 4, 2, 2, 4, 2>(a, s);
+    case 0: return launch<L, LW, false, 2, 2, 4, 4, 2, PF>(a, s);
+    case 1: return launch<L, LW, false, 2, 2, 2, 4, 2, PF>(a, s);
+    case 2: return launch<L, LW, false, 2, 2, 4, 2, 2, PF>(a, s);
+    case 3: return launch<L, LW, false, 2, 2, 2, 2, 4, PF>(a, s);
+    case 4: return launch<L, LW, false, 2, 4, 4, 2, 2, PF>(a, s);
+    case 5: return launch<L, LW, false, 4, 2, 2, 4, 2, PF>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
+  }
+}
+
+template <int PF>
+static int dispatch_limbs(int cfg, bool smallc, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s) {
+  if (wlimbs == 1) {
+    switch (limbs) {
+      case 1: return launch_cfg<1, 1, PF>(cfg, smallc, a, s);
+      case 2: return launch_cfg<2, 1, PF>(cfg, smallc, a, s);
+      default: return launch_cfg<3, 1, PF>(cfg, smallc, a, s);
+    }
+  }
+  if (wlimbs == 3) return launch_cfg<3, 3, PF>(cfg, smallc, a, s);
+  switch (limbs) {
+    case 1: return launch_cfg<1, 2, PF>(cfg, smallc, a, s);
+    case 2: return launch_cfg<2, 2, PF>(cfg, smallc, a, s);
+    default: return launch_cfg<3, 2, PF>(cfg, smallc, a, s);
   }
 }
 
@@ -769,6 +883,11 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
   a.wplane = (long long)cout * a.K;
   a.relu = relu ? 1 : 0;
   a.has_offset = (offset && wlimbs == 1) ? 1 : 0;
+  static const int ablate_env = [] {
+    const char* e = std::getenv("SMPQ_ABLATE");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.ablate = ablate_env;
   hipStream_t s = (hipStream_t)stream;
   if (tile_cfg < 0) {
     const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
@@ -777,19 +896,8 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
   if (tile_cfg >= kNumTileCfgs) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   if (limbs < 1 || limbs > 3) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: limbs must be 1, 2 or 3");
   a.inv_qmax = 1.f / (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f));
-  if (wlimbs == 1) {
-    switch (limbs) {
-      case 1: return launch_cfg<1, 1>(tile_cfg, smallc, a, s);
-      case 2: return launch_cfg<2, 1>(tile_cfg, smallc, a, s);
-      default: return launch_cfg<3, 1>(tile_cfg, smallc, a, s);
-    }
-  }
-  if (wlimbs == 3) return launch_cfg<3, 3>(tile_cfg, smallc, a, s);
-  switch (limbs) {
-    case 1: return launch_cfg<1, 2>(tile_cfg, smallc, a, s);
-    case 2: return launch_cfg<2, 2>(tile_cfg, smallc, a, s);
-    default: return launch_cfg<3, 2>(tile_cfg, smallc, a, s);
-  }
+  if (tile_cfg >= kNumBaseCfgs) return dispatch_limbs<1>(tile_cfg - kNumBaseCfgs, smallc, limbs, wlimbs, a, s);
+  return dispatch_limbs<2>(tile_cfg, smallc, limbs, wlimbs, a, s);
 }
 
 extern "C" int smpq_conv2d_fwd_ex(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
@@ -817,7 +925,7 @@ extern "C" int smpq_conv2d_num_tile_configs(void) { return kNumTileCfgs; }
 extern "C" int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads) {
   if (cfg < 0 || cfg >= kNumTileCfgs || !bm || !bn || !threads)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_tile_config: bad arguments");
-  const TileCfg& t = kTileCfgs[cfg];
+  const TileCfg& t = kTileCfgs[cfg % kNumBaseCfgs];
   *bm = 16 * t.wm * t.wavesm;
   *bn = 16 * t.wn * t.wavesn;
   *threads = 64 * t.wavesm * t.wavesn;

@@ -35,6 +35,20 @@ from .qconv import QConv2d, stats
 
 _MODE = ["static"]
 HEADROOM = 2.0
+# images per pass through the network: a chunk's inter-layer activations (int8 limb planes) stay
+# resident in the 256 MiB Infinity Cache between producer and consumer instead of round-tripping
+# HBM; every image is independent, so chunking changes no result (fc runs once on all features)
+import os as _os
+CHUNK = [int(_os.environ.get("SMPQ_CHUNK", "256"))]
+# replay the static-range forward from a captured HIP graph (one launch instead of ~60 kernels
+# with their Python/ctypes host cost); recaptured when weights, BN, ranges or shapes change
+USE_GRAPH = [_os.environ.get("SMPQ_GRAPH", "1") != "0"]
+stats.setdefault("graph_captures", 0)
+stats.setdefault("graph_replays", 0)
+
+
+def set_chunk(n):
+    CHUNK[0] = max(1, int(n))
 stats.setdefault("calibrations", 0)
 stats.setdefault("overflow_reruns", 0)
 
@@ -161,7 +175,9 @@ def run_conv(conv, bn, act, relu, residual=None, want_amax=True, ctx=None, want_
                                residual=residual, relu=relu, y_absmax=yam, residual_q=res_q,
                                residual_range=res_rng)
         if ctx is not None and ctx.record is not None and yam is not None:
-            ctx.record[id(conv)] = yam
+            prev = ctx.record.get(id(conv))
+            m = yam.amax().reshape(1)
+            ctx.record[id(conv)] = m if prev is None else torch.maximum(prev, m)
         return Act(f32=y, amax=yam)
     yam = torch.zeros(n, dtype=torch.float32, device=conv.weight.device) if want_amax else None
     # geometry the kernel does not cover: the reference's fp32 arithmetic on MIOpen
@@ -227,13 +243,27 @@ def _blocks(model):
     return [b for layer in (model.layer1, model.layer2, model.layer3, model.layer4) for b in layer]
 
 
-def _forward(model, x, ctx):
+def _features(model, x, ctx):
     act = stem_forward(model, x)
     blocks = _blocks(model)
     for i, blk in enumerate(blocks):
         act = block_forward(blk, act, ctx, last=(i == len(blocks) - 1))
-    feat = act.f32.mean(dim=(1, 2))
-    return model.fc(feat)
+    return act.f32.mean(dim=(1, 2))
+
+
+def _forward(model, x, ctx):
+    n = x.shape[0]
+    c = CHUNK[0]
+    if n <= c:
+        return model.fc(_features(model, x, ctx))
+    feats = []
+    for s in range(0, n, c):
+        if ctx is not None:
+            ctx.n = min(c, n - s)
+        feats.append(_features(model, x[s:s + c], ctx))
+    if ctx is not None:
+        ctx.n = n
+    return model.fc(torch.cat(feats))
 
 
 def _signature(model):
@@ -252,7 +282,7 @@ def calibrate(model, x):
     y = _forward(model, x, ctx)
     keys = list(ctx.record)
     if keys:
-        maxima = torch.stack([ctx.record[k].amax() for k in keys]).cpu().tolist()
+        maxima = torch.cat([ctx.record[k] for k in keys]).cpu().tolist()
         old = getattr(model, "_smpq_ranges", None)
         ranges = {}
         for k, v in zip(keys, maxima):
@@ -265,6 +295,40 @@ def calibrate(model, x):
     return y
 
 
+def _static_eager(model, x, cal):
+    ctx = Ctx(x.shape[0], x.device, ranges=cal[0], cache=cal[2])
+    y = _forward(model, x, ctx)
+    return y, ctx.overflow
+
+
+def _graph_forward(model, x, cal):
+    """Static forward through a captured HIP graph; returns (logits, overflow flag tensor)."""
+    from . import ops
+    key = (tuple(x.shape), x.dtype, x.device, cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]))
+    entry = getattr(model, "_smpq_graph", None)
+    if entry is None or entry[0] != key:
+        model._smpq_graph = None
+        y, ovf = _static_eager(model, x, cal)  # warm every cache outside the capture
+        if int(ovf.item()) != 0:
+            return y, ovf
+        static_x = x.clone()
+        g = torch.cuda.CUDAGraph()
+        ctx = Ctx(x.shape[0], x.device, ranges=cal[0], cache=cal[2])
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):
+            ctx.overflow = torch.zeros(1, dtype=torch.int32, device=x.device)
+            y_static = _forward(model, static_x, ctx)
+        model._smpq_graph = (key, g, static_x, ctx, y_static)
+        stats["graph_captures"] += 1
+        return y, ovf
+    _, g, static_x, ctx, y_static = entry
+    if x.data_ptr() != static_x.data_ptr():
+        static_x.copy_(x)
+    g.replay()
+    stats["graph_replays"] += 1
+    return y_static.clone(), ctx.overflow
+
+
 def forward_fused(model, x):
     """Eval-mode forward of an smpq ResNet on the GPU; returns logits [n, num_classes]."""
     if _MODE[0] == "dynamic":
@@ -272,9 +336,11 @@ def forward_fused(model, x):
     cal = getattr(model, "_smpq_ranges", None)
     if cal is None or cal[1] != _signature(model):
         return calibrate(model, x)
-    ctx = Ctx(x.shape[0], x.device, ranges=cal[0], cache=cal[2])
-    y = _forward(model, x, ctx)
-    if int(ctx.overflow.item()) == 0:  # one sync: results are never silently clamped
+    if USE_GRAPH[0] and not torch.cuda.is_current_stream_capturing():
+        y, ovf = _graph_forward(model, x, cal)
+    else:
+        y, ovf = _static_eager(model, x, cal)
+    if int(ovf.item()) == 0:  # one sync: results are never silently clamped
         return y
     stats["overflow_reruns"] += 1
     return calibrate(model, x)

@@ -180,7 +180,8 @@ _TILES = {}
 
 
 def tile_configs():
-    """{cfg: (BM, BN, threads)} of the conv kernel's block tiles."""
+    """{cfg: (BM, BN, threads)} of the conv kernel's block tiles (configs 6..11 repeat 0..5 with
+    one K step of global-load prefetch instead of two)."""
     if not _TILES:
         lib = _lib.load()
         import ctypes
@@ -264,9 +265,9 @@ _TUNED = {}
 
 
 def _tile_fits(cfg, limbs, wlimbs=1, smallc=False):
-    if smallc and cfg not in (2, 3):
-        return False
     bm, bn, nt = tile_configs()[cfg]
+    if smallc and not (bn == 64 and nt == 256):  # the cin == 4 loader exists for these tiles only
+        return False
     waves = nt // 64
     smin = max(0, limbs + wlimbs - 4)  # low-digit passes skipped by the kernel (see conv.hip)
     return (limbs + wlimbs - 1 - smin) * (bm // 16) * (bn // 16) // waves * 4 <= 128

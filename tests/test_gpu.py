@@ -282,6 +282,7 @@ def test_model_logits_vs_reference(gpu, case, arch, assign, batch, limbs, mode):
     x = torch.randn(batch, 3, 224, 224, generator=torch.Generator().manual_seed(1))
     ops.set_act_limbs(limbs)
     engine.set_range_mode(mode)
+    engine.USE_GRAPH[0] = False  # count launches of one eager forward (graphs: test_graph_replay_*)
     try:
         xg = x.to(gpu)
         with torch.no_grad():
@@ -297,6 +298,7 @@ def test_model_logits_vs_reference(gpu, case, arch, assign, batch, limbs, mode):
     finally:
         ops.set_act_limbs(2)
         engine.set_range_mode("static")
+        engine.USE_GRAPH[0] = True
     ref = g[case + "/logits"].astype(np.float64)
     err = np.abs(y - ref).max()
     rel = err / np.abs(ref).max()
@@ -540,3 +542,42 @@ def test_static_ranges_overflow_falls_back_to_dynamic(gpu):
         y_big_dyn = net(5 * x)
         engine.set_range_mode("static")
     assert torch.equal(y_big, y_big_dyn)
+
+
+@pytest.mark.parametrize("mode", ["dynamic", "static"])
+def test_chunked_forward_identical(gpu, mode):
+    """Infinity-Cache batch chunking changes no result (per-image independence)."""
+    from smpq import engine
+    net = build_model(gpu, "resnet50", "r50_mixed")
+    x = torch.randn(12, 3, 224, 224, generator=torch.Generator().manual_seed(13)).to(gpu)
+    engine.set_range_mode(mode)
+    old = engine.CHUNK[0]
+    try:
+        with torch.no_grad():
+            engine.set_chunk(64)
+            net(x)  # calibrates in static mode
+            a = net(x)
+            engine.set_chunk(5)
+            b = net(x)
+    finally:
+        engine.set_chunk(old)
+        engine.set_range_mode("static")
+    assert torch.equal(a, b)
+
+
+def test_graph_replay_matches_eager(gpu):
+    from smpq import engine, stats
+    net = build_model(gpu, "resnet50", "r50_mixed")
+    x = torch.randn(6, 3, 224, 224, generator=torch.Generator().manual_seed(14)).to(gpu)
+    x2 = torch.randn(6, 3, 224, 224, generator=torch.Generator().manual_seed(15)).to(gpu)
+    with torch.no_grad():
+        engine.USE_GRAPH[0] = False
+        net(x)  # calibrate
+        e1, e2 = net(x), net(x2)
+        engine.USE_GRAPH[0] = True
+        c0, r0 = stats["graph_captures"], stats["graph_replays"]
+        g1 = net(x)   # capture
+        g2 = net(x2)  # replay with new input
+        g3 = net(x)   # replay
+    assert stats["graph_captures"] == c0 + 1 and stats["graph_replays"] == r0 + 2
+    assert torch.equal(g1, e1) and torch.equal(g2, e2) and torch.equal(g3, e1)
