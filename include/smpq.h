@@ -162,9 +162,21 @@ int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int
                       int8_t* yq, float yq_range, int32_t* overflow, const int8_t* residual_q,
                       float residual_range, int tile_cfg, smpq_stream_t stream);
 
-/* Tile configurations of smpq_conv2d_fwd (for autotuning): count, and BM x BN / threads. */
+/* Tile configurations of smpq_conv2d_fwd (for autotuning): count, and BM (pixels) x BN (output
+ * channels) / threads. Every configuration gives bitwise-identical results. */
 int smpq_conv2d_num_tile_configs(void);
 int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads);
+
+/* Kernel family of a tile configuration:
+ *   SMPQ_TILE_REGSTAGE         register-staged loader, cin % 64 == 0
+ *   SMPQ_TILE_REGSTAGE_SMALLC  register-staged loader, also cin == 4 (the stem)
+ *   SMPQ_TILE_LDS_DMA          LDS-DMA loader; cin % 64 == 0, cout % 16 == 0, every operand and
+ *                              output plane < 2 GiB
+ * (negative: error code). */
+#define SMPQ_TILE_REGSTAGE 0
+#define SMPQ_TILE_REGSTAGE_SMALLC 1
+#define SMPQ_TILE_LDS_DMA 2
+int smpq_conv2d_tile_kind(int cfg);
 
 /* Workspace the conv needs (none today; kept for ABI stability). */
 size_t smpq_conv2d_workspace_bytes(int n, int h, int w, int cin, int cout, int kh, int kw,

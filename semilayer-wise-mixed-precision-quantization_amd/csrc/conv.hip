@@ -32,54 +32,11 @@
 #include <cstdlib>
 #include <string>
 
-#include "common.h"
+#include "conv_common.h"
 
 namespace smpq {
 
-constexpr int kKStep = 64;     // K per MFMA (i8 16x16x64)
 constexpr int kRowBytes = 80;  // LDS row stride for a 64-byte K slice (+16 B pad vs conflicts)
-
-struct ConvArgs {
-  const int8_t* xq;      // [L][n][h][w][cin] activation limb planes
-  long long plane;       // elements per activation plane
-  const float* x_absmax; // [n]
-  const int8_t* codes;   // [LW][cout][K] weight limb planes
-  long long wplane;      // elements per weight plane (cout*K)
-  const int32_t* w_off;  // [cout] (LW == 1 only) or NULL
-  const float* col_scale;
-  const float* col_shift;
-  const float* residual;   // fp32 NHWC residual, or NULL
-  const int8_t* res_q;     // [L][M][cout] residual limb planes (static range), or NULL
-  float res_scale;         // residual value = res_scale * sum_l 256^l digit_l
-  float* y;              // fp32 NHWC output, or NULL
-  float* y_absmax;
-  int8_t* yq;            // [L][M][cout] output limb planes (static range), or NULL
-  float yq_inv;          // QMAX / range of the output quantizer
-  int32_t* overflow;     // set to 1 when |y| exceeded the static range (then clamped)
-  int n, h, w, cin, cout, kh, kw, stride, pad, ho, wo;
-  int M, K, ksteps, cchunks;
-  int relu, has_offset;
-  float inv_qmax;
-  int ablate;  // diagnostics only (SMPQ_ABLATE): 1 no operand loads, 2 no MFMA, 4 no output stores,
-               // 8 no residual loads. Results are wrong with any bit set; never set in production.
-};
-
-template <int L>
-__device__ __forceinline__ void split_limbs(int q, int* d) {
-  // balanced base-256 digits, each in [-128, 127]
-#pragma unroll
-  for (int l = 0; l < L - 1; ++l) {
-    const int lo = ((q + 128) & 255) - 128;
-    d[l] = lo;
-    q = (q - lo) >> 8;
-  }
-  d[L - 1] = q;
-}
-
-template <int L>
-__device__ __host__ constexpr float act_qmax() {
-  return L == 1 ? 127.f : (L == 2 ? 32512.f : 8323072.f);
-}
 
 // Block = WAVES_M x WAVES_N waves; each wave owns WM x WN 16x16 subtiles.
 template <int L, int LW, bool SMALLC, int WAVES_M, int WAVES_N, int WM, int WN, int MINW, int PF>
@@ -159,17 +116,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
   typedef v4i BSet[LW][BROWS];
 
   auto load_global = [&](int ks, ASet& ra, BSet& rb) {
-    if (a.ablate & 1) {
-#pragma unroll
-      for (int l = 0; l < L; ++l)
-#pragma unroll
-        for (int i = 0; i < AR; ++i) ra[l][i] = v4i{ks, 0, 0, 0};
-#pragma unroll
-      for (int lw = 0; lw < LW; ++lw)
-#pragma unroll
-        for (int j = 0; j < BROWS; ++j) rb[lw][j] = v4i{ks, 1, 0, 0};
-      return;
-    }
     if constexpr (SMALLC) {
       // 16 taps x 4 channels per K step; this thread's piece = taps 16*ks + 4*piece + 0..3
       const int taps = a.kh * a.kw;
@@ -257,7 +203,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
   const bool do_off = (LW == 1) && a.has_offset;
 
   auto compute = [&](int buf) {
-    if (a.ablate & 2) return;
     v4i bf[LW][WN];
 #pragma unroll
     for (int lw = 0; lw < LW; ++lw)
@@ -359,7 +304,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
   constexpr int V4 = BN / 4;  // float4 per tile row
   const bool vec_ok = (a.cout & 3) == 0;
   __syncthreads();
-  if (a.res_q && !(a.ablate & 8)) {
+  if (a.res_q) {
     // residual from the block input's int8 limb planes, 16 channels (16 B per limb) per item;
     // every load of this thread is issued before the first use (constant trip count, unrolled)
     constexpr int V16 = BN / 16;
@@ -399,8 +344,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
             for (int k = 0; k < 4; ++k) q[k] += (int)(int8_t)(wd >> (8 * k)) * limbw;
             limbw *= 256;
           }
-          v = make_float4(a.res_scale * (float)q[0], a.res_scale * (float)q[1], a.res_scale * (float)q[2],
-                          a.res_scale * (float)q[3]);
+          v = make_float4(__fmul_rn(a.res_scale, (float)q[0]), __fmul_rn(a.res_scale, (float)q[1]),
+                          __fmul_rn(a.res_scale, (float)q[2]), __fmul_rn(a.res_scale, (float)q[3]));
         } else if (m < a.M) {  // ragged channel tail (cout % 16 != 0): bytewise
           const int8_t* src = a.res_q + (size_t)m * a.cout;
           float t[4] = {0.f, 0.f, 0.f, 0.f};
@@ -412,7 +357,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
               q += (int)src[l * rplane + c] * limbw;
               limbw *= 256;
             }
-            t[k] = a.res_scale * (float)q;
+            t[k] = __fmul_rn(a.res_scale, (float)q);
           }
           v = make_float4(t[0], t[1], t[2], t[3]);
         }
@@ -420,7 +365,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
       }
     }
     __syncthreads();
-  } else if (a.residual && !(a.ablate & 8)) {
+  } else if (a.residual) {
     for (int e = tid; e < BM * V4; e += NT) {
       const int r = e / V4, c4 = e - (e / V4) * V4;
       const int m = m0 + r, col = n0 + 4 * c4;
@@ -460,12 +405,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
         for (int s = 0; s < NACC; ++s) {
           int t = acc[s][i][j][r];
           if (SMIN == 0 && s < L) t += coloff[j] * rsum[s];  // offsets only exist for LW == 1
-          v += (float)t * limbw;
+          v = __fmaf_rn((float)t, limbw, v);
           limbw *= 256.f;
         }
-        float out = v * (rscale * colscale[j]) + colshift[j];
+        float out = affine(v, rscale, colscale[j], colshift[j]);
         float* tp = &tile[rloc * TS + cloc];
-        if (a.residual || a.res_q) out += *tp;
+        if (a.residual || a.res_q) out = __fadd_rn(out, *tp);
         if (a.relu) out = fmaxf(out, 0.f);
         *tp = out;
         if (n0 + cloc < a.cout) rmax = fmaxf(rmax, fabsf(out));
@@ -482,7 +427,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
   }
   __syncthreads();
   bool ovf = false;
-  if (a.y && !(a.ablate & 4)) {
+  if (a.y) {
     for (int e = tid; e < BM * V4; e += NT) {
       const int r = e / V4, c4 = e - (e / V4) * V4;
       const int m = m0 + r, col = n0 + 4 * c4;
@@ -499,7 +444,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
       }
     }
   }
-  if (a.yq && !(a.ablate & 4)) {
+  if (a.yq) {
     // fused activation quantizer of the NEXT conv's input (static per-layer range):
     // 16 channels per item -> one 16-B store per limb plane
     constexpr float qmax = act_qmax<L>();
@@ -518,7 +463,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
         for (int l = 0; l < L; ++l) word[l][g] = 0u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          float qf = rintf(vals[k] * a.yq_inv);
+          float qf = rintf(__fmul_rn(vals[k], a.yq_inv));
           ovf |= (col + 4 * g + k < a.cout) && fabsf(qf) > qmax;
           qf = fminf(fmaxf(qf, -qmax), qmax);
           int d[L];
@@ -883,19 +828,18 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
   a.wplane = (long long)cout * a.K;
   a.relu = relu ? 1 : 0;
   a.has_offset = (offset && wlimbs == 1) ? 1 : 0;
-  static const int ablate_env = [] {
-    const char* e = std::getenv("SMPQ_ABLATE");
-    return e ? std::atoi(e) : 0;
-  }();
-  a.ablate = ablate_env;
   hipStream_t s = (hipStream_t)stream;
   if (tile_cfg < 0) {
     const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
     tile_cfg = heuristic_cfg(limbs + wlimbs - 1 - smin, M, cout, a.K, smallc);
   }
-  if (tile_cfg >= kNumTileCfgs) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
+  if (tile_cfg >= kNumTileCfgs + glds_num_cfgs()) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   if (limbs < 1 || limbs > 3) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: limbs must be 1, 2 or 3");
   a.inv_qmax = 1.f / (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f));
+  if (tile_cfg >= kNumTileCfgs) {
+    if (smallc) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: LDS-DMA tile configs need cin % 64 == 0");
+    return launch_glds(tile_cfg - kNumTileCfgs, limbs, wlimbs, a, s);
+  }
   if (tile_cfg >= kNumBaseCfgs) return dispatch_limbs<1>(tile_cfg - kNumBaseCfgs, smallc, limbs, wlimbs, a, s);
   return dispatch_limbs<2>(tile_cfg, smallc, limbs, wlimbs, a, s);
 }
@@ -920,11 +864,23 @@ extern "C" int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, i
                             col_scale, col_shift, residual, relu, limbs, y, y_absmax, tile_cfg, stream);
 }
 
-extern "C" int smpq_conv2d_num_tile_configs(void) { return kNumTileCfgs; }
+extern "C" int smpq_conv2d_num_tile_configs(void) { return kNumTileCfgs + glds_num_cfgs(); }
+
+extern "C" int smpq_conv2d_tile_kind(int cfg) {
+  if (cfg < 0 || cfg >= kNumTileCfgs + glds_num_cfgs())
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_tile_kind: bad config");
+  if (cfg >= kNumTileCfgs) return SMPQ_TILE_LDS_DMA;
+  const int b = cfg % kNumBaseCfgs;
+  return (b == 2 || b == 3) ? SMPQ_TILE_REGSTAGE_SMALLC : SMPQ_TILE_REGSTAGE;
+}
 
 extern "C" int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads) {
-  if (cfg < 0 || cfg >= kNumTileCfgs || !bm || !bn || !threads)
+  if (cfg < 0 || cfg >= kNumTileCfgs + glds_num_cfgs() || !bm || !bn || !threads)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_tile_config: bad arguments");
+  if (cfg >= kNumTileCfgs) {
+    glds_cfg_info(cfg - kNumTileCfgs, bm, bn, threads);
+    return SMPQ_OK;
+  }
   const TileCfg& t = kTileCfgs[cfg % kNumBaseCfgs];
   *bm = 16 * t.wm * t.wavesm;
   *bn = 16 * t.wn * t.wavesn;

@@ -51,6 +51,7 @@ _PROTOS = {
                                _vp, _i, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, ctypes.c_float, _i, _vp]),
     "smpq_conv2d_num_tile_configs": (_i, []),
     "smpq_conv2d_tile_config": (_i, [_i, _vp, _vp, _vp]),
+    "smpq_conv2d_tile_kind": (_i, [_i]),
     "smpq_conv2d_workspace_bytes": (ctypes.c_size_t, [_i] * 10),
     "smpq_debug_mfma_i8": (_i, [_vp, _vp, _vp, _vp]),
 }

@@ -190,7 +190,21 @@ def tile_configs():
             _lib.check(lib.smpq_conv2d_tile_config(c, ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(nt)),
                        "smpq_conv2d_tile_config")
             _TILES[c] = (bm.value, bn.value, nt.value)
+            kind = lib.smpq_conv2d_tile_kind(c)
+            if kind < 0:
+                _lib.check(kind, "smpq_conv2d_tile_kind")
+            _KINDS[c] = kind
     return _TILES
+
+
+TILE_REGSTAGE, TILE_REGSTAGE_SMALLC, TILE_LDS_DMA = 0, 1, 2  # include/smpq.h SMPQ_TILE_*
+_KINDS = {}
+
+
+def tile_kind(cfg):
+    """Kernel family of a tile config (TILE_REGSTAGE / TILE_REGSTAGE_SMALLC / TILE_LDS_DMA)."""
+    tile_configs()
+    return _KINDS[cfg]
 
 
 def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
@@ -264,13 +278,19 @@ AUTOTUNE = [os.environ.get("SMPQ_AUTOTUNE", "1") != "0"]
 _TUNED = {}
 
 
-def _tile_fits(cfg, limbs, wlimbs=1, smallc=False):
+def _tile_fits(cfg, limbs, wlimbs=1, smallc=False, cout=None):
     bm, bn, nt = tile_configs()[cfg]
-    if smallc and not (bn == 64 and nt == 256):  # the cin == 4 loader exists for these tiles only
+    kind = _KINDS[cfg]
+    if smallc and kind != TILE_REGSTAGE_SMALLC:  # the cin == 4 loader exists for these tiles only
         return False
     waves = nt // 64
     smin = max(0, limbs + wlimbs - 4)  # low-digit passes skipped by the kernel (see conv.hip)
-    return (limbs + wlimbs - 1 - smin) * (bm // 16) * (bn // 16) // waves * 4 <= 128
+    accs = (limbs + wlimbs - 1 - smin) * (bm // 16) * (bn // 16) // waves * 4
+    if kind == TILE_LDS_DMA:
+        if cout is not None and cout % 16:
+            return False
+        return accs < 128 or (accs == 128 and limbs == 1)  # (128 at 2 activation limbs spills)
+    return accs <= 128
 
 
 def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
@@ -287,19 +307,22 @@ def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, 
     if cfg is None and AUTOTUNE[0] and not torch.cuda.is_current_stream_capturing():
         best = None
         for c in tile_configs():
-            if not _tile_fits(c, limbs, wlimbs, cin == 4):
+            if not _tile_fits(c, limbs, wlimbs, cin == 4, cout):
                 continue
             times = []
-            for rep in range(3):
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record()
-                conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
-                         residual=residual, relu=relu, y_absmax=y_absmax, out=out, tile_cfg=c,
-                         emit_range=emit_range, overflow=overflow, want_f32=want_f32,
-                         residual_q=residual_q, residual_range=residual_range)
-                e1.record()
-                times.append((e0, e1))
+            try:
+                for rep in range(3):
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
+                             residual=residual, relu=relu, y_absmax=y_absmax, out=out, tile_cfg=c,
+                             emit_range=emit_range, overflow=overflow, want_f32=want_f32,
+                             residual_q=residual_q, residual_range=residual_range)
+                    e1.record()
+                    times.append((e0, e1))
+            except _lib.SmpqError:
+                continue  # this family does not take the shape (e.g. a plane over 2 GiB)
             torch.cuda.synchronize()
             t = min(a.elapsed_time(b) for a, b in times[1:])
             if best is None or t < best[0]:

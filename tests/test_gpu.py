@@ -224,16 +224,64 @@ def test_all_tile_configs_bitwise_identical(gpu, shape, limbs):
     shift = torch.linspace(-1, 1, cout, device=gpu)
     outs = []
     for c in ops.tile_configs():
-        if not ops._tile_fits(c, limbs):
+        if not ops._tile_fits(c, limbs, 1, False, cout):
             continue
         ya = torch.zeros(3, device=gpu)
         y = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, residual=res, relu=True,
                          y_absmax=ya, tile_cfg=c)
         outs.append((c, y, ya))
     assert len(outs) >= 3
+    assert any(ops.tile_kind(c) == ops.TILE_LDS_DMA for c, _, _ in outs)
     for c, y, ya in outs[1:]:
         assert torch.equal(y, outs[0][1]), c
         assert torch.equal(ya, outs[0][2]), c
+
+
+@pytest.mark.parametrize("range_frac", [2.0, 0.5])
+@pytest.mark.parametrize("limbs", [1, 2, 3])
+@pytest.mark.parametrize("shape", [(64, 256, 1, 1, 20), (128, 64, 3, 2, 17), (64, 80, 3, 1, 9)],
+                         ids=lambda s: "c%d_o%d_k%d_s%d_h%d" % s)
+def test_static_outputs_identical_across_tiles(gpu, shape, limbs, range_frac):
+    """Static-range epilogue: limb-plane output (next conv's input), limb-plane residual, overflow
+    flag and fp32 output agree bitwise across every tile config of both kernel families, and the
+    emitted digits are clamp(rne(y * QMAX / range))."""
+    from smpq import ops
+    cin, cout, k, s, h = shape
+    wd, step, codes, offset = make_layer(gpu, cin, cout, k, seed=cin + 5 * cout)
+    g = torch.Generator().manual_seed(11)
+    x = torch.relu(torch.randn(3, h, h, cin, generator=g)).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, limbs)
+    ho = (h + 2 * (k // 2) - k) // s + 1
+    rq = ops.act_quantize(torch.randn(3, ho, ho, cout, generator=g).clamp(-4, 4).to(gpu),
+                          torch.full((3,), 4.0, device=gpu), limbs)
+    shift = torch.linspace(-1, 1, cout, device=gpu)
+    ref = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, relu=True,
+                       residual_q=rq, residual_range=4.0)
+    rng = float(ref.abs().max()) * range_frac
+    outs = []
+    for c in ops.tile_configs():
+        if not ops._tile_fits(c, limbs, 1, False, cout):
+            continue
+        ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+        y, yq = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, relu=True, tile_cfg=c,
+                             emit_range=rng, overflow=ovf, want_f32=True, residual_q=rq, residual_range=4.0)
+        outs.append((c, y, yq, ovf))
+    assert any(ops.tile_kind(c) == ops.TILE_LDS_DMA for c, *_ in outs)
+    c0, y0, yq0, ovf0 = outs[0]
+    assert torch.equal(y0, ref)
+    for c, y, yq, ovf in outs[1:]:
+        assert torch.equal(y, y0), c
+        assert torch.equal(yq, yq0), c
+        assert torch.equal(ovf, ovf0), c
+    qmax = LIMB_QMAX[limbs]
+    inv = np.float32(qmax) / np.float32(rng)  # the kernel's yq_inv, in float32 like the C side
+    qf = np.rint(y0.cpu().numpy().astype(np.float32) * inv)
+    q = sum(yq0[l].cpu().numpy().astype(np.int64) * 256 ** l for l in range(limbs))
+    assert (yq0.cpu().numpy().astype(np.int64) >= -128).all()
+    np.testing.assert_array_equal(q, np.clip(qf, -qmax, qmax).astype(np.int64))
+    assert int(ovf0.item()) == int((np.abs(qf) > qmax).any())
+    assert int(ovf0.item()) == (1 if range_frac < 1 else 0)
 
 
 def test_conv_offsets_exercised(gpu):
@@ -458,9 +506,12 @@ def test_conv_weight_limbs_vs_emulation(gpu, limbs, wlimbs):
     ho = (h + 2 - k) // s + 1
     res = torch.randn(3, ho, ho, cout, generator=g).to(gpu)
     outs = []
+    kinds = set()
     for c in ops.tile_configs():
-        if ops._tile_fits(c, limbs, wlimbs):
+        if ops._tile_fits(c, limbs, wlimbs, False, cout):
             outs.append(ops.conv2d_q(xq, am, codes, None, k, k, s, 1, cs, sh, residual=res, relu=True, tile_cfg=c))
+            kinds.add(ops.tile_kind(c))
+    assert ops.TILE_LDS_DMA in kinds
     assert len(outs) >= 1 and all(torch.equal(o, outs[0]) for o in outs)
     wq = codes.cpu().numpy().reshape(wlimbs, cout, k, k, cin)
     rscale = (am.cpu().numpy() * np.float32(1.0 / LIMB_QMAX[limbs])).astype(np.float64)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Time single quantized-conv launches of representative R50 shapes (B=256) per tile config.
-Diagnostics only. usage: python tools/conv_microbench.py [limbs] [static|dynamic]
+Diagnostics only. usage: python tools/conv_microbench.py [limbs] [static|dynamic] [shape-substr] [cfg,...]
 With SMPQ_ABLATE set (see conv.hip) the numbers are ablations (wrong results)."""
 import os
 import sys
@@ -18,6 +18,8 @@ from smpq import ops  # noqa: E402
 L = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 static = (sys.argv[2] if len(sys.argv) > 2 else "static") == "static"
 B = 256
+ONLY = sys.argv[3] if len(sys.argv) > 3 else None
+CFGS = [int(c) for c in sys.argv[4].split(",")] if len(sys.argv) > 4 else None
 SHAPES = [  # name, cin, cout, k, stride, hin, residual
     ("c1_256_64_56", 256, 64, 1, 1, 56, False),
     ("c2_64_64_56", 64, 64, 3, 1, 56, False),
@@ -28,6 +30,8 @@ SHAPES = [  # name, cin, cout, k, stride, hin, residual
 ]
 dev = torch.device("cuda")
 for name, cin, cout, k, s, h, res in SHAPES:
+    if ONLY and ONLY not in name:
+        continue
     g = torch.Generator(device=dev).manual_seed(0)
     w = torch.randn(cout, cin, k, k, device=dev, generator=g) * 0.05
     step = ops.quantize_channels_(w.reshape(cout, -1), [6] * cout)
@@ -44,7 +48,7 @@ for name, cin, cout, k, s, h, res in SHAPES:
     byt = B * h * h * cin * L + B * ho * ho * cout * L * (2 if res else 1)
     out = []
     for c in ops.tile_configs():
-        if not ops._tile_fits(c, L, 1):
+        if not ops._tile_fits(c, L, 1) or (CFGS is not None and c not in CFGS):
             continue
         kw = dict(emit_range=8.0, overflow=ovf, want_f32=False) if static else {}
         if res:
