@@ -29,7 +29,19 @@ namespace smpq {
 
 namespace {
 
+// Diagnostic builds only (tools/ablate_glds.sh compiles separate libraries with -DSMPQ_DIAG_ABLATE=N;
+// results are wrong with any bit set): 1 no residual loads, 2 no limb-plane stores, 4 no operand
+// DMA, 8 no MFMA.
+#ifndef SMPQ_DIAG_ABLATE
+#define SMPQ_DIAG_ABLATE 0
+#endif
+constexpr int kAblate = SMPQ_DIAG_ABLATE;
+
 constexpr unsigned kOOB = 0x80000000u;  // a buffer offset past every range we build (< 2^31 B)
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// byte offset of an fp32 element offset (kOOB stays out of range: 4 * kOOB would wrap to 0)
+__device__ __forceinline__ unsigned f32_off(unsigned e) { return e == kOOB ? kOOB : 4u * e; }
 
 __device__ __forceinline__ v4i make_rsrc(const void* base, long long bytes) {
   const unsigned long long b = reinterpret_cast<unsigned long long>(base);
@@ -56,6 +68,21 @@ __device__ __forceinline__ void dma16(unsigned lds, v4i rsrc, unsigned voff, uns
 }
 
 __device__ __forceinline__ int swz(int row) { return (4 - (row >> 2)) & 3; }
+
+// 4 x 4 transpose of (lane group g = lane >> 4, register c): afterwards group g register c holds
+// what group c register g held. v_permlane32_swap exchanges the upper half of its first operand
+// with the lower half of its second, v_permlane16_swap the odd rows of the first with the even
+// rows of the second.
+__device__ __forceinline__ void transpose4(unsigned& w0, unsigned& w1, unsigned& w2, unsigned& w3) {
+  const auto a = __builtin_amdgcn_permlane32_swap(w0, w2, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(w1, w3, false, false);
+  const auto c = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+  const auto d = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+  w0 = c[0];
+  w1 = c[1];
+  w2 = d[0];
+  w3 = d[1];
+}
 
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)reinterpret_cast<unsigned long long>(p);
@@ -94,7 +121,7 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
   constexpr int STAGE = NPIECE * 1024;
   constexpr int WSLOTS = (WPIECES + NW - 1) / NW;
   constexpr int ASLOTS = (APIECES + NW - 1) / NW;
-  __shared__ __attribute__((aligned(1024))) int8_t lds[2 * STAGE];
+  extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // 1 stage (ksteps == 1) or 2
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -154,13 +181,13 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 #pragma unroll
     for (int s = 0; s < WSLOTS; ++s) {
       const int p = wave + NW * s;
-      if (p < WPIECES) dma16(sb + p * 1024, wrs, wsrc[s], __builtin_amdgcn_readfirstlane(ks * kKStep));
+      if (p < WPIECES && !(kAblate & 4)) dma16(sb + p * 1024, wrs, wsrc[s], __builtin_amdgcn_readfirstlane(ks * kKStep));
     }
     const int tapoff = (kr * a.w + kc) * a.cin + c0;
 #pragma unroll
     for (int s = 0; s < ASLOTS; ++s) {
       const int p = wave + NW * s;
-      if (p < APIECES) {
+      if (p < APIECES && !(kAblate & 4)) {
         const int l = p / (BP / 16);
         const bool ok = (unsigned)(aih[s] + kr) < (unsigned)a.h && (unsigned)(aiw[s] + kc) < (unsigned)a.w;
         const unsigned voff = ok ? (unsigned)(apix[s] + tapoff) : kOOB;
@@ -187,6 +214,73 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
   // fragment read offset inside a piece (same for every piece)
   const int frow = lane & 15;
   const int rd = frow * 64 + 16 * ((lane >> 4) ^ swz(frow));
+
+  // Output coordinates of this lane: channels chan[i] + 0..3 of pixel mrow[j]; ooff = element
+  // offset in an NHWC plane, or kOOB (then buffer loads read 0 and buffer stores are dropped).
+  int mrow[WP];
+  bool mok[WP];
+#pragma unroll
+  for (int j = 0; j < WP; ++j) {
+    const int m = m0 + (wp * WP + j) * 16 + frow;
+    mok[j] = m < a.M;
+    mrow[j] = mok[j] ? m : 0;
+  }
+  int chan[WC];
+#pragma unroll
+  for (int i = 0; i < WC; ++i) chan[i] = n0 + (wc * WC + i) * 16 + 4 * (lane >> 4);
+  unsigned ooff[WC][WP];
+#pragma unroll
+  for (int i = 0; i < WC; ++i)
+#pragma unroll
+    for (int j = 0; j < WP; ++j)  // cout % 16 == 0: the 4 channels are valid together
+      ooff[i][j] = (mok[j] && chan[i] < a.cout) ? (unsigned)(mrow[j] * a.cout + chan[i]) : kOOB;
+  const long long oplane = (long long)a.M * a.cout;
+  // With 4k channel blocks per wave the limb planes move as 16-B pieces: after a lane-group
+  // transpose (transpose4) lane group g owns the 16 channels of block 4q + g of its pixel, so
+  // one wave-instruction covers 64 contiguous bytes of each of 16 pixel rows.
+  constexpr bool TR = (WC % 4) == 0;
+  constexpr int NQ = TR ? WC / 4 : 1;
+  unsigned qoff[NQ][WP];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      const int c16 = n0 + (wc * WC + 4 * q + (lane >> 4)) * 16;
+      qoff[q][j] = (TR && mok[j] && c16 < a.cout) ? (unsigned)(mrow[j] * a.cout + c16) : kOOB;
+    }
+
+  // residual limb planes: issued now, consumed in the epilogue (latency hidden behind the K loop)
+  int rq[WC][WP][L];
+  if constexpr (TR) {
+    if (a.res_q) {
+      const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.res_q), 0, (int)(L * oplane),
+                                                         0x00020000);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int j = 0; j < WP; ++j)
+#pragma unroll
+          for (int l = 0; l < L; ++l) {
+            const v4u v = (kAblate & 1) ? v4u{qoff[q][j], 0u, 0u, 0u}
+                                        : __builtin_amdgcn_raw_buffer_load_b128(rrs, qoff[q][j],
+                                                                                (unsigned)((long long)l * oplane), 0);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) rq[4 * q + c][j][l] = (int)v[c];
+          }
+    }
+  } else if (a.res_q) {
+    const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.res_q), 0, (int)(L * oplane),
+                                                       0x00020000);
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j)
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+          rq[i][j][l] = (kAblate & 1) ? (int)ooff[i][j]
+                                      : (int)__builtin_amdgcn_raw_buffer_load_b32(rrs, ooff[i][j],
+                                                                                  (unsigned)((long long)l * oplane), 0);
+  }
 
   int kr = 0, kc = 0, c0 = 0;
   issue(0, 0, 0, 0, 0);
@@ -234,7 +328,7 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
     for (int l = 0; l < L; ++l)
 #pragma unroll
       for (int lw = 0; lw < LW; ++lw) {
-        if (l + lw < SMIN) continue;  // compile-time: skipped low-digit product
+        if (l + lw < SMIN || (kAblate & 8)) continue;  // compile-time: skipped low-digit product
 #pragma unroll
         for (int i = 0; i < WC; ++i)
 #pragma unroll
@@ -244,8 +338,24 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
       }
   }
 
-  // ---- epilogue: straight from the accumulators --------------------------------------------
-  // lane: channels ch(i) + r (r = 0..3) of pixel m(j)
+  // ---- epilogue: straight from the accumulators, in phases (uniform branches per phase) -----
+  if constexpr (TR) {
+    if (a.res_q) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int j = 0; j < WP; ++j)
+#pragma unroll
+          for (int l = 0; l < L; ++l) {
+            unsigned w0 = rq[4 * q][j][l], w1 = rq[4 * q + 1][j][l], w2 = rq[4 * q + 2][j][l], w3 = rq[4 * q + 3][j][l];
+            transpose4(w0, w1, w2, w3);
+            rq[4 * q][j][l] = (int)w0;
+            rq[4 * q + 1][j][l] = (int)w1;
+            rq[4 * q + 2][j][l] = (int)w2;
+            rq[4 * q + 3][j][l] = (int)w3;
+          }
+    }
+  }
   if (do_off) {
 #pragma unroll
     for (int l = 0; l < L; ++l)
@@ -257,133 +367,148 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
         rs[l][j] = s;
       }
   }
-  int mrow[WP];
   float rscale[WP];
-  bool mok[WP];
 #pragma unroll
-  for (int j = 0; j < WP; ++j) {
-    const int m = m0 + (wp * WP + j) * 16 + frow;
-    mok[j] = m < a.M;
-    mrow[j] = mok[j] ? m : 0;
-    rscale[j] = mok[j] ? a.x_absmax[m / hw_out] * a.inv_qmax : 0.f;
-  }
-  int chan[WC];
-  bool cok[WC];
-  float4 cs[WC], csh[WC];
-  int4 coff[WC];
+  for (int j = 0; j < WP; ++j) rscale[j] = mok[j] ? a.x_absmax[mrow[j] / hw_out] * a.inv_qmax : 0.f;
+
+  float o[WC][WP][4];
 #pragma unroll
   for (int i = 0; i < WC; ++i) {
-    chan[i] = n0 + (wc * WC + i) * 16 + 4 * (lane >> 4);
-    cok[i] = chan[i] < a.cout;  // cout % 16 == 0: the 4 channels are valid together
-    const int c = cok[i] ? chan[i] : 0;
-    cs[i] = *reinterpret_cast<const float4*>(a.col_scale + c);
-    csh[i] = *reinterpret_cast<const float4*>(a.col_shift + c);
-    coff[i] = do_off ? *reinterpret_cast<const int4*>(a.w_off + c) : int4{0, 0, 0, 0};
-  }
-
-  // residual: all loads issued before any use
-  const long long oplane = (long long)a.M * a.cout;
-  int rq[WC][WP][L];
-  float4 rf[WC][WP];
-  if (a.res_q) {
-    const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.res_q), 0, (int)(L * oplane),
-                                                       0x00020000);
+    const int c = chan[i] < a.cout ? chan[i] : 0;
+    const float4 cs = *reinterpret_cast<const float4*>(a.col_scale + c);
+    const float4 csh = *reinterpret_cast<const float4*>(a.col_shift + c);
+    const int4 coff = do_off ? *reinterpret_cast<const int4*>(a.w_off + c) : int4{0, 0, 0, 0};
+    const float csr[4] = {cs.x, cs.y, cs.z, cs.w};
+    const float shr[4] = {csh.x, csh.y, csh.z, csh.w};
+    const int cor[4] = {coff.x, coff.y, coff.z, coff.w};
 #pragma unroll
-    for (int i = 0; i < WC; ++i)
-#pragma unroll
-      for (int j = 0; j < WP; ++j) {
-        const unsigned off = (mok[j] && cok[i]) ? (unsigned)(mrow[j] * a.cout + chan[i]) : kOOB;
-#pragma unroll
-        for (int l = 0; l < L; ++l)
-          rq[i][j][l] = (int)__builtin_amdgcn_raw_buffer_load_b32(rrs, off, (unsigned)((long long)l * oplane), 0);
-      }
-  } else if (a.residual) {
-    const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.residual), 0, (int)(4 * oplane),
-                                                       0x00020000);
-#pragma unroll
-    for (int i = 0; i < WC; ++i)
-#pragma unroll
-      for (int j = 0; j < WP; ++j) {
-        const unsigned off = (mok[j] && cok[i]) ? (unsigned)(4 * (mrow[j] * a.cout + chan[i])) : kOOB;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rrs, off, 0, 0);
-        rf[i][j] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
-                               __uint_as_float(v[3]));
-      }
-  }
-
-  constexpr float qmax = act_qmax<L>();
-  float vmax = 0.f;  // max |y| over this lane's valid outputs (static-range overflow test)
-  float pmax[WP];    // per-pixel max |y| (dynamic per-image range)
-#pragma unroll
-  for (int j = 0; j < WP; ++j) pmax[j] = 0.f;
-#pragma unroll
-  for (int i = 0; i < WC; ++i) {
-#pragma unroll
-    for (int j = 0; j < WP; ++j) {
-      const bool ok = mok[j] && cok[i];
-      float o[4];
+    for (int j = 0; j < WP; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int rsum[L];
-#pragma unroll
-        for (int l = 0; l < L; ++l) rsum[l] = rs[l][j];
-        const int co = r == 0 ? coff[i].x : (r == 1 ? coff[i].y : (r == 2 ? coff[i].z : coff[i].w));
         float v = 0.f;
         float limbw = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
 #pragma unroll
         for (int s = 0; s < NACC; ++s) {
           int tq = acc[s][i][j][r];
-          if (SMIN == 0 && s < L && do_off) tq += co * rsum[s];
+          if (SMIN == 0 && s < L && do_off) tq += cor[r] * rs[s][j];
           v = __fmaf_rn((float)tq, limbw, v);
           limbw *= 256.f;
         }
-        const float csr = r == 0 ? cs[i].x : (r == 1 ? cs[i].y : (r == 2 ? cs[i].z : cs[i].w));
-        const float shr = r == 0 ? csh[i].x : (r == 1 ? csh[i].y : (r == 2 ? csh[i].z : csh[i].w));
-        float out = affine(v, rscale[j], csr, shr);
-        if (a.res_q) {
+        o[i][j][r] = affine(v, rscale[j], csr[r], shr[r]);
+      }
+  }
+  if (a.res_q) {
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
           int q = 0;
 #pragma unroll
           for (int l = L - 1; l >= 0; --l) q = q * 256 + __builtin_amdgcn_sbfe(rq[i][j][l], 8 * r, 8);
-          out = __fadd_rn(out, __fmul_rn(a.res_scale, (float)q));
-        } else if (a.residual) {
-          const float rv = r == 0 ? rf[i][j].x : (r == 1 ? rf[i][j].y : (r == 2 ? rf[i][j].z : rf[i][j].w));
-          out = __fadd_rn(out, rv);
+          o[i][j][r] = __fadd_rn(o[i][j][r], __fmul_rn(a.res_scale, (float)q));
         }
-        if (a.relu) out = fmaxf(out, 0.f);
-        o[r] = out;
-      }
-      if (ok) {
-        const float am = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
-        pmax[j] = fmaxf(pmax[j], am);
-        vmax = fmaxf(vmax, am);
-      }
-      const long long oidx = (long long)mrow[j] * a.cout + chan[i];
-      if (a.y && ok) *reinterpret_cast<float4*>(a.y + oidx) = make_float4(o[0], o[1], o[2], o[3]);
-      if (a.yq && ok) {
-        int q[4];
+  } else if (a.residual) {
+    const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.residual), 0, (int)(4 * oplane),
+                                                       0x00020000);
+    v4u rv[WC][WP];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) q[r] = (int)fminf(fmaxf(rintf(__fmul_rn(o[r], a.yq_inv)), -qmax), qmax);
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j) rv[i][j] = __builtin_amdgcn_raw_buffer_load_b128(rrs, f32_off(ooff[i][j]), 0, 0);
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[i][j][r] = __fadd_rn(o[i][j][r], __uint_as_float(rv[i][j][r]));
+  }
+  if (a.relu) {
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[i][j][r] = fmaxf(o[i][j][r], 0.f);
+  }
+  if (a.y) {
+    const auto yrs = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)(4 * oplane), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j) {
+        const v4u v = {__float_as_uint(o[i][j][0]), __float_as_uint(o[i][j][1]), __float_as_uint(o[i][j][2]),
+                       __float_as_uint(o[i][j][3])};
+        __builtin_amdgcn_raw_buffer_store_b128(v, yrs, f32_off(ooff[i][j]), 0, 0);
+      }
+  }
+  constexpr float qmax = act_qmax<L>();
+  if (a.yq) {
+    // fused quantizer of the next conv's input (static range): one dword per limb plane
+    const auto qrs = __builtin_amdgcn_make_buffer_rsrc(a.yq, 0, (int)(L * oplane), 0x00020000);
+    float vmax = 0.f;
+    unsigned wq[WC][WP][L];
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j) {
+        int q[4];
+        float am = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          q[r] = (int)fminf(fmaxf(rintf(__fmul_rn(o[i][j][r], a.yq_inv)), -qmax), qmax);
+          am = fmaxf(am, fabsf(o[i][j][r]));
+        }
+        vmax = ooff[i][j] != kOOB ? fmaxf(vmax, am) : vmax;
         unsigned wd[L];
-        if constexpr (L >= 1) wd[0] = pack_bytes(q[0], q[1], q[2], q[3], 0);
+        wd[0] = pack_bytes(q[0], q[1], q[2], q[3], 0);
         if constexpr (L >= 2)
           wd[1] = pack_bytes(digit_src<1>(q[0]), digit_src<1>(q[1]), digit_src<1>(q[2]), digit_src<1>(q[3]), 1);
         if constexpr (L >= 3)
           wd[2] = pack_bytes(digit_src<2>(q[0]), digit_src<2>(q[1]), digit_src<2>(q[2]), digit_src<2>(q[3]), 2);
 #pragma unroll
-        for (int l = 0; l < L; ++l) *reinterpret_cast<unsigned*>(a.yq + l * oplane + oidx) = wd[l];
+        for (int l = 0; l < L; ++l) wq[i][j][l] = wd[l];
       }
+    if constexpr (TR) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int j = 0; j < WP; ++j)
+#pragma unroll
+          for (int l = 0; l < L; ++l) {
+            unsigned w0 = wq[4 * q][j][l], w1 = wq[4 * q + 1][j][l], w2 = wq[4 * q + 2][j][l], w3 = wq[4 * q + 3][j][l];
+            transpose4(w0, w1, w2, w3);
+            if (!(kAblate & 2) || w0 == 0x12345679u)
+              __builtin_amdgcn_raw_buffer_store_b128(v4u{w0, w1, w2, w3}, qrs, qoff[q][j],
+                                                     (unsigned)((long long)l * oplane), 0);
+          }
+    } else {
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+#pragma unroll
+        for (int j = 0; j < WP; ++j)
+#pragma unroll
+          for (int l = 0; l < L; ++l)
+            if (!(kAblate & 2) || wq[i][j][l] == 0x12345679u)
+              __builtin_amdgcn_raw_buffer_store_b32(wq[i][j][l], qrs, ooff[i][j], (unsigned)((long long)l * oplane), 0);
     }
-  }
-  if (a.yq) {
+    // |rne(y * inv)| is monotone in |y|: one test on the lane's max
     const bool ovf = rintf(__fmul_rn(vmax, a.yq_inv)) > qmax;
     if (__any(ovf) && lane == 0) atomicMax(a.overflow, 1);
   }
   if (a.y_absmax) {
-    // per pixel: reduce over the 4 lane groups holding its channels
+    float pmax[WP];  // per pixel max |y| over this lane's channels, then over the 4 lane groups
 #pragma unroll
     for (int j = 0; j < WP; ++j) {
-      pmax[j] = fmaxf(pmax[j], __shfl_xor(pmax[j], 16, kWave));
-      pmax[j] = fmaxf(pmax[j], __shfl_xor(pmax[j], 32, kWave));
+      float am = 0.f;
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+        if (ooff[i][j] != kOOB)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) am = fmaxf(am, fabsf(o[i][j][r]));
+      am = fmaxf(am, __shfl_xor(am, 16, kWave));
+      pmax[j] = fmaxf(am, __shfl_xor(am, 32, kWave));
     }
     const int mfirst = m0 + wp * WP * 16;
     const int mlast = min(mfirst + WP * 16, a.M) - 1;
@@ -416,6 +541,9 @@ constexpr GldsCfg kGlds[] = {
     {1, 4, 4, 2},  // 4:  64 ch x 128 px
     {4, 1, 2, 4},  // 5: 128 ch x  64 px (each wave 32 ch x all 64 px)
     {2, 2, 4, 4},  // 6: 128 ch x 128 px (<= 2 accumulator sets)
+    {4, 1, 4, 2},  // 7: 256 ch x  32 px (whole 256-B output rows per block: wide 1x1 expansions)
+    {4, 1, 4, 1},  // 8: 256 ch x  16 px
+    {2, 2, 4, 1},  // 9: 128 ch x  32 px
 };
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
@@ -438,8 +566,14 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
     const long mt = (a.M + BP - 1) / BP;
     const long nt = (a.cout + BC - 1) / BC;
     if (mt * nt > 0x7fffffffL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
-    hipLaunchKernelGGL((qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, 2>), dim3((unsigned)(mt * nt)),
-                       dim3(64 * WAVES_C * WAVES_P), 0, stream, a);
+    constexpr int STAGE = (LW * (BC / 16) + L * (BP / 16)) * 1024;
+    auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, 2>;
+    static const hipError_t attr =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 2 * STAGE);
+    if (attr != hipSuccess) return check_hip(attr, "qconv_glds_kernel LDS attribute");
+    // a single K step needs one LDS stage: twice the blocks per CU for the 1x1 convs with cin 64
+    const int lds_bytes = (a.ksteps > 1 ? 2 : 1) * STAGE;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(mt * nt)), dim3(64 * WAVES_C * WAVES_P), lds_bytes, stream, a);
     return check_hip(hipGetLastError(), "qconv_glds_kernel launch");
   }
 }
@@ -454,6 +588,9 @@ static int launch_cfg(int cfg, const ConvArgs& a, hipStream_t s) {
     case 4: return launch_one<L, LW, 1, 4, 4, 2>(a, s);
     case 5: return launch_one<L, LW, 4, 1, 2, 4>(a, s);
     case 6: return launch_one<L, LW, 2, 2, 4, 4>(a, s);
+    case 7: return launch_one<L, LW, 4, 1, 4, 2>(a, s);
+    case 8: return launch_one<L, LW, 4, 1, 4, 1>(a, s);
+    case 9: return launch_one<L, LW, 2, 2, 4, 1>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   }
 }

@@ -14,10 +14,10 @@ for d in sys.argv[1:]:
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            if "qconv_kernel" not in name:
+            if "qconv" not in name:
                 continue
-            m = re.search(r"qconv_kernel<([^>]*)>", name)
-            key = m.group(1).replace(" ", "") if m else name
+            m = re.search(r"(qconv\w*)<([^>]*)>", name)
+            key = (m.group(1) + "<" + m.group(2).replace(" ", "") + ">") if m else name
             key += " vgpr=%s lds=%s" % (r["VGPR_Count"], r["LDS_Block_Size"])
             vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
             dur[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
