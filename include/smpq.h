@@ -162,6 +162,32 @@ int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int
                       int8_t* yq, float yq_range, int32_t* overflow, const int8_t* residual_q,
                       float residual_range, int tile_cfg, smpq_stream_t stream);
 
+/* ---- space-to-depth stem (the 7x7 / stride 2 / pad 3 conv1 of resnet.py:143) -------------------
+ * The stem runs as a 4x4 / stride 1 conv over 16-channel "space-to-depth" pixels (each a 2x2
+ * block of the image with up to 4 channels), so every 64-byte K step of the int8 GEMM is one
+ * tap row of whole 16-byte pixels. Results are bitwise identical to smpq_conv2d_fwd_q on the
+ * 4-channel planes of smpq_image_quantize with the smpq_pack_weights_ex codes (same per-channel
+ * fixed point, exact integer accumulation).
+ *
+ * smpq_image_quantize_s2d: x fp32 NCHW [n][c <= 4][h][w], h and w even ->
+ *   out int8 [limbs][n][h/2][w/2][16], channel (dy*2 + dx)*4 + ci = x[ci][2i + dy][2j + dx]
+ *   quantized with the per-image absmax like smpq_image_quantize (zero for ci >= c).
+ * smpq_pack_weights_s2d: w fp32 [cout][cin <= 4][7][7] -> codes int8 [wlimbs][cout][256] (K order
+ *   [ty][tx][dy][dx][ci], original tap (2 ty + dy - 1, 2 tx + dx - 1), zero outside 7x7) in
+ *   per-channel fixed point (wlimbs 2 / 3 = 16 / 24 bits) with scale wscale [cout];
+ *   status[2] counts the channels coded. (No quantized-code mode: the stem is never quantized.)
+ * smpq_stem_conv_s2d_q: as smpq_conv2d_fwd_q with the stem geometry (h, w = the ORIGINAL image
+ *   size; output [n][h/2][w/2][cout] NHWC), no residual; cout % 16 == 0; tile_cfg one of the
+ *   SMPQ_TILE_LDS_DMA configs with 64 output channels per block, or -1. */
+int smpq_image_quantize_s2d(const float* x, int n, int c, int h, int w, const float* absmax, int limbs,
+                            int8_t* out, smpq_stream_t stream);
+int smpq_pack_weights_s2d(const float* w, int cout, int cin, int wlimbs, int8_t* codes, float* wscale,
+                          int32_t* status, smpq_stream_t stream);
+int smpq_stem_conv_s2d_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, const int8_t* codes,
+                         int wlimbs, int cout, const float* col_scale, const float* col_shift, int relu,
+                         int limbs, float* y, float* y_absmax, int8_t* yq, float yq_range, int32_t* overflow,
+                         int tile_cfg, smpq_stream_t stream);
+
 /* Tile configurations of smpq_conv2d_fwd (for autotuning): count, and BM (pixels) x BN (output
  * channels) / threads. Every configuration gives bitwise-identical results. */
 int smpq_conv2d_num_tile_configs(void);

@@ -29,6 +29,7 @@
 // v_mfma_i32_16x16x64_i8. Global -> register prefetch of K step k+1 overlaps the MFMAs of step
 // k; one LDS double buffer, one barrier per K step; the epilogue reuses the LDS arena as an fp32
 // output tile so residual loads and output stores are whole 16-B pieces of contiguous rows.
+#include <algorithm>
 #include <cstdlib>
 #include <string>
 
@@ -574,6 +575,53 @@ __global__ __launch_bounds__(256) void image_quantize_kernel(const float* __rest
   }
 }
 
+// NCHW fp32 images (c <= 4 channels, even h and w) -> L int8 limb planes in space-to-depth
+// layout [n][h/2][w/2][16], channel (dy * 2 + dx) * 4 + c = pixel (2i + dy, 2j + dx), channel c
+// (zero for c >= c_in): the stem's 7x7/2 conv becomes a 4x4/1 conv over 16-channel pixels whose
+// 64-B K steps are whole tap rows (smpq_stem_conv_s2d_q). One thread = one 16-channel pixel.
+template <int L>
+__global__ __launch_bounds__(256) void image_quantize_s2d_kernel(const float* __restrict__ x, int n, int c, int h,
+                                                                 int w, const float* __restrict__ absmax,
+                                                                 int8_t* __restrict__ out, long long plane) {
+  const float qmax = act_qmax<L>();
+  const int h2 = h / 2, w2 = w / 2;
+  const long long total = (long long)n * h2 * w2;
+  for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < total;
+       p += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(p % w2);
+    const long long t = p / w2;
+    const int i = (int)(t % h2);
+    const int img = (int)(t / h2);
+    const float am = absmax[img];
+    const float inv = am > 0.f ? qmax / am : 0.f;
+    unsigned int word[L][4];
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) word[l][g] = 0u;
+    for (int ch = 0; ch < c; ++ch) {
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+        const float2 v = *reinterpret_cast<const float2*>(x + (((size_t)img * c + ch) * h + 2 * i + dy) * w + 2 * j);
+        const float vals[2] = {v.x, v.y};
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) {
+          const float qf = fminf(fmaxf(rintf(vals[dx] * inv), -qmax), qmax);
+          int d[L];
+          split_limbs<L>((int)qf, d);
+          const int g = dy * 2 + dx;  // byte 4 g + ch of the 16
+#pragma unroll
+          for (int l = 0; l < L; ++l) word[l][g] |= (unsigned int)(d[l] & 255) << (8 * ch);
+        }
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+      *reinterpret_cast<v4i*>(out + l * plane + 16 * p) =
+          v4i{(int)word[l][0], (int)word[l][1], (int)word[l][2], (int)word[l][3]};
+  }
+}
+
 // 3x3 / stride 2 / pad 1 max pool (resnet.py:147) on NHWC fp32, fused with the activation
 // quantizer of its output (per-image range absmax = max of the pool input: max-pooling a
 // non-negative ReLU output keeps the per-image maximum). Optional fp32 output.
@@ -784,6 +832,7 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
   if (wlimbs == 3 && limbs != 3)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: 3 weight limbs are built for 3 activation limbs only");
   ConvArgs a;
+  a.s2d = 0;
   a.xq = xq;
   a.plane = (long long)n * h * w * cin;
   a.x_absmax = x_absmax;
@@ -931,6 +980,72 @@ extern "C" int smpq_image_quantize(const float* x, int n, int c, int h, int w, c
     default: return fail(SMPQ_E_INVALID, "smpq_image_quantize: limbs must be 1, 2 or 3");
   }
   return check_hip(hipGetLastError(), "image_quantize_kernel launch");
+}
+
+extern "C" int smpq_image_quantize_s2d(const float* x, int n, int c, int h, int w, const float* absmax, int limbs,
+                                       int8_t* out, smpq_stream_t stream) {
+  if (!x || !absmax || !out || n <= 0 || c <= 0 || c > 4 || h <= 1 || w <= 1 || (h & 1) || (w & 1))
+    return fail(SMPQ_E_INVALID, "smpq_image_quantize_s2d: need 1..4 channels and even h, w");
+  const long long total = (long long)n * (h / 2) * (w / 2);
+  const long long plane = total * 16;
+  const dim3 grid((unsigned)std::min<long long>((total + 255) / 256, 65535));
+  hipStream_t s = (hipStream_t)stream;
+  switch (limbs) {
+    case 1: hipLaunchKernelGGL(image_quantize_s2d_kernel<1>, grid, dim3(256), 0, s, x, n, c, h, w, absmax, out, plane); break;
+    case 2: hipLaunchKernelGGL(image_quantize_s2d_kernel<2>, grid, dim3(256), 0, s, x, n, c, h, w, absmax, out, plane); break;
+    case 3: hipLaunchKernelGGL(image_quantize_s2d_kernel<3>, grid, dim3(256), 0, s, x, n, c, h, w, absmax, out, plane); break;
+    default: return fail(SMPQ_E_INVALID, "smpq_image_quantize_s2d: limbs must be 1, 2 or 3");
+  }
+  return check_hip(hipGetLastError(), "image_quantize_s2d_kernel launch");
+}
+
+extern "C" int smpq_stem_conv_s2d_q(const int8_t* xq, const float* x_absmax, int n, int h, int w,
+                                    const int8_t* codes, int wlimbs, int cout, const float* col_scale,
+                                    const float* col_shift, int relu, int limbs, float* y, float* y_absmax,
+                                    int8_t* yq, float yq_range, int32_t* overflow, int tile_cfg,
+                                    smpq_stream_t stream) {
+  if (!xq || !x_absmax || !codes || !col_scale || !col_shift || (!y && !yq))
+    return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: null pointer");
+  if (yq && (!overflow || !(yq_range > 0.f)))
+    return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: yq needs overflow flag and a positive range");
+  if (n <= 0 || h <= 1 || w <= 1 || (h & 1) || (w & 1) || cout <= 0)
+    return fail(SMPQ_E_SHAPE, "smpq_stem_conv_s2d_q: bad shape (h, w must be even)");
+  if (limbs < 1 || limbs > 3) return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: limbs must be 1, 2 or 3");
+  if (tile_cfg < 0) tile_cfg = kNumTileCfgs;  // LDS-DMA 64 x 64
+  if (tile_cfg < kNumTileCfgs || tile_cfg >= kNumTileCfgs + glds_num_cfgs())
+    return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: the stem runs on the LDS-DMA tile configs");
+  ConvArgs a = {};
+  a.s2d = 1;
+  a.xq = xq;
+  a.x_absmax = x_absmax;
+  a.codes = codes;
+  a.col_scale = col_scale;
+  a.col_shift = col_shift;
+  a.y = y;
+  a.y_absmax = y_absmax;
+  a.yq = yq;
+  a.overflow = overflow;
+  a.yq_inv = yq ? (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f)) / yq_range : 0.f;
+  a.n = n;
+  a.h = h / 2;  // space-to-depth geometry: 4x4 taps, stride 1, pad 2 (top / left; bottom / right by range)
+  a.w = w / 2;
+  a.cin = 16;
+  a.cout = cout;
+  a.kh = a.kw = 4;
+  a.stride = 1;
+  a.pad = 2;
+  a.ho = (h + 2 * 3 - 7) / 2 + 1;  // the original 7x7 / stride 2 / pad 3 output
+  a.wo = (w + 2 * 3 - 7) / 2 + 1;
+  a.M = n * a.ho * a.wo;
+  a.K = 256;
+  a.ksteps = 4;
+  a.cchunks = 1;
+  a.plane = (long long)n * a.h * a.w * 16;
+  a.wplane = (long long)cout * a.K;
+  a.relu = relu ? 1 : 0;
+  a.inv_qmax = 1.f / (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f));
+  if ((long long)n * a.ho * a.wo > 0x7fffffffLL) return fail(SMPQ_E_SHAPE, "smpq_stem_conv_s2d_q: tensor too large");
+  return launch_glds(tile_cfg - kNumTileCfgs, limbs, wlimbs, a, (hipStream_t)stream);
 }
 
 extern "C" int smpq_maxpool_quantize(const float* x, int n, int h, int w, int c, const float* absmax, int limbs,

@@ -29,6 +29,7 @@ struct ConvArgs {
   int M, K, ksteps, cchunks;
   int relu, has_offset;
   float inv_qmax;
+  int s2d;  // space-to-depth stem (smpq_stem_conv_s2d_q): cin 16, 4 x 4 taps, K step = one tap row
 };
 
 template <int L>

@@ -108,7 +108,10 @@ __device__ __forceinline__ unsigned pack_bytes(int b0, int b1, int b2, int b3, i
 
 }  // namespace
 
-template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW>
+// S2D: the space-to-depth stem. The image is stored as 16-channel pixels ([2x2 block][4 ch]) and
+// the 7x7/2 conv is a 4x4/1 conv over them (pad 2, zero taps where the 8x8 extension falls
+// outside 7x7); a 64-B K step is one tap row: lane chunk c = the 16 channels of tap column c.
+template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D>
 __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kernel(ConvArgs a) {
   constexpr int NW = WAVES_C * WAVES_P;
   constexpr int BC = 16 * WC * WAVES_C;  // channels per block tile
@@ -164,9 +167,16 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
       const int img = m / hw_out;
       const int rem = m - img * hw_out;
       const int oh = rem / a.wo, ow = rem - (rem / a.wo) * a.wo;
-      aih[s] = oh * a.stride - a.pad;
-      aiw[s] = ow * a.stride - a.pad;
-      apix[s] = ((img * a.h + aih[s]) * a.w + aiw[s]) * a.cin + 16 * pchunk;
+      if constexpr (S2D) {
+        aih[s] = oh - a.pad;
+        aiw[s] = ow - a.pad + pchunk;  // this lane's tap column, fixed over the K steps
+        apix[s] = ((img * a.h + aih[s]) * a.w + aiw[s]) * 16;
+        if ((unsigned)aiw[s] >= (unsigned)a.w) aih[s] = -(1 << 28);
+      } else {
+        aih[s] = oh * a.stride - a.pad;
+        aiw[s] = ow * a.stride - a.pad;
+        apix[s] = ((img * a.h + aih[s]) * a.w + aiw[s]) * a.cin + 16 * pchunk;
+      }
     } else {
       aih[s] = -(1 << 28);  // never inside the image
       aiw[s] = 0;
@@ -189,8 +199,14 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
       const int p = wave + NW * s;
       if (p < APIECES && !(kAblate & 4)) {
         const int l = p / (BP / 16);
-        const bool ok = (unsigned)(aih[s] + kr) < (unsigned)a.h && (unsigned)(aiw[s] + kc) < (unsigned)a.w;
-        const unsigned voff = ok ? (unsigned)(apix[s] + tapoff) : kOOB;
+        unsigned voff;
+        if constexpr (S2D) {
+          const bool ok = (unsigned)(aih[s] + ks) < (unsigned)a.h;
+          voff = ok ? (unsigned)(apix[s] + ks * a.w * 16) : kOOB;
+        } else {
+          const bool ok = (unsigned)(aih[s] + kr) < (unsigned)a.h && (unsigned)(aiw[s] + kc) < (unsigned)a.w;
+          voff = ok ? (unsigned)(apix[s] + tapoff) : kOOB;
+        }
         dma16(sb + (WPIECES + p) * 1024, xrs, voff,
               __builtin_amdgcn_readfirstlane((unsigned)((long long)l * a.plane)));
       }
@@ -556,7 +572,7 @@ void glds_cfg_info(int cfg, int* bm, int* bn, int* threads) {
   *threads = 64 * c.wavesc * c.wavesp;
 }
 
-template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP>
+template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, bool S2D = false>
 static int launch_one(const ConvArgs& a, hipStream_t stream) {
   constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
   if constexpr ((L + LW - 1 - SMIN) * WC * WP * 4 > 128) {
@@ -567,7 +583,7 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
     const long nt = (a.cout + BC - 1) / BC;
     if (mt * nt > 0x7fffffffL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
     constexpr int STAGE = (LW * (BC / 16) + L * (BP / 16)) * 1024;
-    auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, 2>;
+    auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, 2, S2D>;
     static const hipError_t attr =
         hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 2 * STAGE);
     if (attr != hipSuccess) return check_hip(attr, "qconv_glds_kernel LDS attribute");
@@ -595,14 +611,32 @@ static int launch_cfg(int cfg, const ConvArgs& a, hipStream_t s) {
   }
 }
 
+// The stem (cout 64): tiles of 64 output channels only, fixed-point weights (LW = max(2, L)).
+template <int L, int LW>
+static int launch_s2d(int cfg, const ConvArgs& a, hipStream_t s) {
+  switch (cfg) {
+    case 0: return launch_one<L, LW, 2, 2, 2, 2, true>(a, s);
+    case 1: return launch_one<L, LW, 2, 2, 2, 4, true>(a, s);
+    case 3: return launch_one<L, LW, 1, 4, 4, 1, true>(a, s);
+    case 4: return launch_one<L, LW, 1, 4, 4, 2, true>(a, s);
+    default: return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: tile config not built for the stem");
+  }
+}
+
 int launch_glds(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s) {
   // operand and output planes are addressed with 32-bit buffer offsets below kOOB
   const long long lim = 0x7fffff00LL;
-  if (a.cin % kKStep != 0 || a.cout % 16 != 0 || (long long)limbs * a.plane > lim ||
+  if ((!a.s2d && a.cin % kKStep != 0) || a.cout % 16 != 0 || (long long)limbs * a.plane > lim ||
       (long long)wlimbs * a.wplane > lim || (long long)limbs * a.M * a.cout > lim ||
       (a.residual && 4LL * a.M * a.cout > lim))
     return fail(SMPQ_E_INVALID,
                 "smpq_conv2d_fwd: LDS-DMA tile configs need cin % 64 == 0, cout % 16 == 0 and planes < 2 GiB");
+  if (a.s2d) {
+    if (wlimbs == 2 && limbs == 1) return launch_s2d<1, 2>(cfg, a, s);
+    if (wlimbs == 2 && limbs == 2) return launch_s2d<2, 2>(cfg, a, s);
+    if (wlimbs == 3 && limbs == 3) return launch_s2d<3, 3>(cfg, a, s);
+    return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: weight limbs must be max(2, limbs)");
+  }
   if (wlimbs == 1) {
     switch (limbs) {
       case 1: return launch_cfg<1, 1>(cfg, a, s);

@@ -90,7 +90,7 @@ constexpr float kW16Max = 32512.f;    // 2-limb fixed-point code range (127 * 25
 constexpr float kW24Max = 8323072.f;  // 3-limb fixed-point code range (127 * 65536)
 
 __global__ __launch_bounds__(kQThreads) void pack_weights_ex_kernel(
-    const float* __restrict__ w, int cin, int kh, int kw, int cin_pad, int K, int lw,
+    const float* __restrict__ w, int cin, int kh, int kw, int cin_pad, int K, int lw, int s2d,
     const float* __restrict__ step, int8_t* __restrict__ codes, long long wplane,
     int32_t* __restrict__ offset, float* __restrict__ wscale, int32_t* __restrict__ status) {
   __shared__ int smem[4 * kQThreads / kWave];
@@ -153,11 +153,21 @@ __global__ __launch_bounds__(kQThreads) void pack_weights_ex_kernel(
   }
   const bool zero = (lw == 1) && (bad || range_bad);
   for (int k = threadIdx.x; k < K; k += kQThreads) {
-    const int tap = k / cin_pad;
-    const int ci = k - tap * cin_pad;
+    int src = -1;  // index of the weight in the [cin][kh][kw] row, or -1 for a zero code
+    if (s2d) {
+      // space-to-depth stem (smpq_pack_weights_s2d): k = [ty][tx][dy][dx][c] over a 4 x 4 x 16
+      // kernel; original tap (2 ty + dy - 1, 2 tx + dx - 1) of channel c
+      const int t = k >> 4, ch = k & 15;
+      const int kr = 2 * (t >> 2) + (ch >> 3) - 1, kc = 2 * (t & 3) + ((ch >> 2) & 1) - 1, ci = ch & 3;
+      if (ci < cin && kr >= 0 && kr < kh && kc >= 0 && kc < kw) src = ci * taps + kr * kw + kc;
+    } else {
+      const int tap = k / cin_pad;
+      const int ci = k - tap * cin_pad;
+      if (tap < taps && ci < cin) src = ci * taps + tap;
+    }
     int m = 0;
-    if (!zero && tap < taps && ci < cin) {
-      const float v = row[ci * taps + tap];
+    if (!zero && src >= 0) {
+      const float v = row[src];
       // fixed point: round in double (at 24 bits an fp32 quotient cannot round exactly)
       if (fixed) m = (int)fmin(fmax(rint((double)v / (double)sc), -(double)wmax), (double)wmax);
       else m = (int)rintf(__fdiv_rn(v, sc)) - o;
@@ -231,7 +241,7 @@ extern "C" int smpq_pack_weights(const float* w, int cout, int cin, int kh, int 
     return fail(SMPQ_E_INVALID, "smpq_pack_weights: bad arguments");
   const int K = cin * kh * kw;
   hipLaunchKernelGGL(pack_weights_ex_kernel, dim3(cout), dim3(kQThreads), 0, (hipStream_t)stream, w,
-                     cin, kh, kw, cin, K, 1, step, codes, (long long)cout * K, offset, (float*)nullptr,
+                     cin, kh, kw, cin, K, 1, 0, step, codes, (long long)cout * K, offset, (float*)nullptr,
                      status);
   return check_hip(hipGetLastError(), "pack_weights_ex_kernel launch");
 }
@@ -255,7 +265,19 @@ extern "C" int smpq_pack_weights_ex(const float* w, int cout, int cin, int kh, i
     return fail(SMPQ_E_SHAPE, "smpq_pack_weights_ex: cin must be <= 4 or a multiple of 64");
   }
   hipLaunchKernelGGL(pack_weights_ex_kernel, dim3(cout), dim3(kQThreads), 0, (hipStream_t)stream, w,
-                     cin, kh, kw, cin_pad, K, wlimbs, step, codes, (long long)cout * K, offset, wscale,
+                     cin, kh, kw, cin_pad, K, wlimbs, 0, step, codes, (long long)cout * K, offset, wscale,
                      status);
+  return check_hip(hipGetLastError(), "pack_weights_ex_kernel launch");
+}
+
+extern "C" int smpq_pack_weights_s2d(const float* w, int cout, int cin, int wlimbs, int8_t* codes, float* wscale,
+                                     int32_t* status, smpq_stream_t stream) {
+  if (!w || !codes || !wscale || !status || cout <= 0 || cin <= 0 || cin > 4)
+    return fail(SMPQ_E_INVALID, "smpq_pack_weights_s2d: bad arguments (cin must be 1..4)");
+  if (wlimbs < 2 || wlimbs > 3) return fail(SMPQ_E_INVALID, "smpq_pack_weights_s2d: wlimbs must be 2 or 3");
+  constexpr int K = 256;  // 4 x 4 taps x 16 space-to-depth channels
+  hipLaunchKernelGGL(pack_weights_ex_kernel, dim3(cout), dim3(kQThreads), 0, (hipStream_t)stream, w, cin, 7, 7,
+                     16, K, wlimbs, 1, (const float*)nullptr, codes, (long long)cout * K, (int32_t*)nullptr,
+                     wscale, status);
   return check_hip(hipGetLastError(), "pack_weights_ex_kernel launch");
 }

@@ -220,14 +220,55 @@ def block_forward(blk, x, ctx=None, last=False):
                     want_f32=last)
 
 
+def stem_s2d_plan(conv, bn):
+    """(codes, col_scale, col_shift) of the stem in space-to-depth form (ops.stem_conv_s2d), or
+    None when conv1 is not the 7x7/2/3 stem on <= 4 channels. Its fp32 weights become per-channel
+    fixed point with max(2, L) limbs, exactly as conv_plan's 'fixed' kind (same codes)."""
+    if not (isinstance(conv, QConv2d) and conv.weight.is_cuda and conv.in_channels <= 4
+            and conv.kernel_size == (7, 7) and conv.stride == (2, 2) and conv.padding == (3, 3)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.out_channels % 16 == 0
+            and not (conv._bits_host > 0).any()):
+        return None
+    key = (conv._pack_key(), _bn_key(bn), None if conv.bias is None else (conv.bias.data_ptr(), conv.bias._version))
+    cache = getattr(conv, "_s2d_cache", None)
+    if cache is not None and cache[0] == key:
+        return cache[1]
+    with torch.no_grad():
+        codes, wscale = ops.pack_weights_s2d(conv.weight.detach().float(), max(2, ops.get_act_limbs()))
+        if bn is not None:
+            a, b = _bn_fold(bn)
+        else:
+            a, b = torch.ones_like(wscale), torch.zeros_like(wscale)
+        if conv.bias is not None:
+            b = b + conv.bias.float() * a
+        plan = (codes, (wscale * a).contiguous(), b.contiguous())
+    conv._s2d_cache = (key, plan)
+    return plan
+
+
 def stem_forward(model, x):
     """conv1 7x7/2 + bn1 + relu + maxpool 3x3/2 (resnet.py:206-209) -> Act of the pooled output."""
     x = x.float().contiguous()
     n = x.shape[0]
+    pool_ok = isinstance(model.maxpool, torch.nn.MaxPool2d) and model.maxpool.kernel_size in (3, (3, 3)) \
+        and model.maxpool.stride in (2, (2, 2)) and model.maxpool.padding in (1, (1, 1))
+    s2d = stem_s2d_plan(model.conv1, model.bn1) if (pool_ok and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0) \
+        else None
+    if s2d is not None:
+        # space-to-depth stem: 16-channel pixels, K steps of whole tap rows (LDS-DMA kernel)
+        codes, col_scale, col_shift = s2d
+        amax_in = ops.act_absmax(x)
+        xq = ops.image_quantize_s2d(x, amax_in)
+        yam = torch.zeros(n, dtype=torch.float32, device=x.device)
+        y = ops.tuned_stem_conv_s2d(xq, amax_in, codes, x.shape[2], x.shape[3], col_scale, col_shift,
+                                    relu=True, y_absmax=yam)
+        stats["hip_conv"] += 1
+        stats["fixed_conv"] += 1
+        model.conv1.last_path = "hip-fixed-s2d"
+        q, f = ops.maxpool_quantize(y, yam, want_f32=True)
+        return Act(f32=f, q=q, amax=yam)
     plan = conv_plan(model.conv1, model.bn1)
-    if plan is not None and x.shape[1] <= 4 and isinstance(model.maxpool, torch.nn.MaxPool2d) \
-            and model.maxpool.kernel_size in (3, (3, 3)) and model.maxpool.stride in (2, (2, 2)) \
-            and model.maxpool.padding in (1, (1, 1)):
+    if plan is not None and x.shape[1] <= 4 and pool_ok:
         amax_in = ops.act_absmax(x)
         xq = ops.image_quantize(x, amax_in)
         stem = run_conv(model.conv1, model.bn1, Act(q=xq, amax=amax_in), relu=True)

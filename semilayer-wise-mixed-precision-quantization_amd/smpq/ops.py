@@ -124,6 +124,95 @@ def image_quantize(x, x_absmax, limbs=None):
     return out
 
 
+def image_quantize_s2d(x, x_absmax, limbs=None):
+    """NCHW fp32 images (c <= 4, even h, w) -> space-to-depth limb planes [limbs, n, h/2, w/2, 16]
+    (channel (dy*2 + dx)*4 + c = pixel (2i+dy, 2j+dx), channel c): the stem's input (stem_conv_s2d)."""
+    limbs = limbs or get_act_limbs()
+    _req(x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous() and x.shape[1] <= 4,
+         "image_quantize_s2d: need contiguous NCHW fp32 with <= 4 channels")
+    n, c, h, w = x.shape
+    _req(h % 2 == 0 and w % 2 == 0, "image_quantize_s2d: h and w must be even")
+    _req(x_absmax.numel() == n and x_absmax.dtype == torch.float32, "image_quantize_s2d: absmax")
+    out = torch.empty(limbs, n, h // 2, w // 2, 16, dtype=torch.int8, device=x.device)
+    lib = _lib.load()
+    with torch.cuda.device(x.device):
+        _lib.check(lib.smpq_image_quantize_s2d(_lib.ptr(x), n, c, h, w, _lib.ptr(x_absmax), int(limbs),
+                                               _lib.ptr(out), _lib.stream_ptr()), "smpq_image_quantize_s2d")
+    return out
+
+
+def pack_weights_s2d(w, wlimbs):
+    """7x7 stem weight fp32 [cout, c <= 4, 7, 7] -> (codes int8 [wlimbs, cout, 256] in the
+    space-to-depth K order, wscale fp32 [cout]) in per-channel fixed point (wlimbs 2 or 3)."""
+    _req(w.is_cuda and w.dtype == torch.float32 and w.dim() == 4 and tuple(w.shape[2:]) == (7, 7)
+         and w.shape[1] <= 4, "pack_weights_s2d: need a CUDA fp32 [cout, <=4, 7, 7] weight")
+    _req(wlimbs in (2, 3), "pack_weights_s2d: wlimbs must be 2 or 3")
+    w = w.contiguous()
+    cout, cin = w.shape[:2]
+    codes = torch.empty(wlimbs, cout, 256, dtype=torch.int8, device=w.device)
+    wscale = torch.empty(cout, dtype=torch.float32, device=w.device)
+    status = torch.zeros(3, dtype=torch.int32, device=w.device)
+    lib = _lib.load()
+    with torch.cuda.device(w.device):
+        _lib.check(lib.smpq_pack_weights_s2d(_lib.ptr(w), cout, cin, int(wlimbs), _lib.ptr(codes), _lib.ptr(wscale),
+                                             _lib.ptr(status), _lib.stream_ptr()), "smpq_pack_weights_s2d")
+    return codes, wscale
+
+
+def stem_conv_s2d(xq, x_absmax, codes, h, w, col_scale, col_shift, relu=True, y_absmax=None, tile_cfg=-1,
+                  emit_range=None, overflow=None, want_f32=True):
+    """The stem conv (7x7/2/3 on the original h x w image) on space-to-depth planes from
+    image_quantize_s2d with pack_weights_s2d codes -> NHWC fp32 y [n, h/2, w/2, cout] (and the
+    next limb planes when emit_range is given: returns (y or None, yq) then)."""
+    limbs, n, h2, w2, c16 = xq.shape
+    _req(c16 == 16 and h2 * 2 == h and w2 * 2 == w, "stem_conv_s2d: planes do not match h, w")
+    wlimbs, cout, K = codes.shape
+    _req(K == 256, "stem_conv_s2d: codes must come from pack_weights_s2d")
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    y = torch.empty(n, ho, wo, cout, dtype=torch.float32, device=xq.device) if want_f32 else None
+    yq = None
+    if emit_range is not None:
+        _req(overflow is not None, "stem_conv_s2d: emit_range needs an overflow flag tensor")
+        yq = torch.empty(limbs, n, ho, wo, cout, dtype=torch.int8, device=xq.device)
+    lib = _lib.load()
+    with torch.cuda.device(xq.device):
+        _lib.check(lib.smpq_stem_conv_s2d_q(
+            _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, _lib.ptr(codes), int(wlimbs), cout, _lib.ptr(col_scale),
+            _lib.ptr(col_shift), 1 if relu else 0, int(limbs), _lib.ptr(y), _lib.ptr(y_absmax), _lib.ptr(yq),
+            float(emit_range or 0.0), _lib.ptr(overflow), int(tile_cfg), _lib.stream_ptr()), "smpq_stem_conv_s2d_q")
+    return y if emit_range is None else (y, yq)
+
+
+def tuned_stem_conv_s2d(xq, x_absmax, codes, h, w, col_scale, col_shift, relu=True, y_absmax=None, **kw):
+    """stem_conv_s2d on the fastest LDS-DMA tile for this shape (bitwise-identical results)."""
+    key = ("stem_s2d", tuple(xq.shape), tuple(codes.shape), h, w, y_absmax is not None,
+           kw.get("emit_range") is not None, kw.get("want_f32", True))
+    cfg = _TUNED.get(key)
+    if cfg is None and AUTOTUNE[0] and not torch.cuda.is_current_stream_capturing():
+        best = None
+        for c in tile_configs():
+            if tile_kind(c) != TILE_LDS_DMA:
+                continue
+            try:
+                evs = []
+                for rep in range(3):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    stem_conv_s2d(xq, x_absmax, codes, h, w, col_scale, col_shift, relu, y_absmax, c, **kw)
+                    e1.record()
+                    evs.append((e0, e1))
+            except _lib.SmpqError:
+                continue  # tile not built for the stem
+            torch.cuda.synchronize()
+            t = min(a.elapsed_time(b) for a, b in evs[1:])
+            if best is None or t < best[0]:
+                best = (t, c)
+        cfg = best[1]
+        _TUNED[key] = cfg
+    return stem_conv_s2d(xq, x_absmax, codes, h, w, col_scale, col_shift, relu, y_absmax,
+                         -1 if cfg is None else cfg, **kw)
+
+
 def maxpool_quantize(x_nhwc, x_absmax, limbs=None, want_f32=True):
     """MaxPool2d(3, 2, 1) on NHWC fp32 fused with the activation quantizer of its output.
     Returns (limb planes [limbs, n, ho, wo, c], fp32 NHWC pooled or None)."""

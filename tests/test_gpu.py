@@ -559,6 +559,52 @@ def test_image_quantize_and_stem_conv(gpu):
 
 
 @pytest.mark.parametrize("limbs", [2, 3])
+@pytest.mark.parametrize("hw", [(40, 36), (224, 224)])
+def test_stem_s2d_bitwise_matches_4ch_stem(gpu, limbs, hw):
+    """The space-to-depth stem (16-channel pixels, 4x4/1 taps) equals the 4-channel 7x7/2 stem
+    bit for bit: same fixed-point codes, exact integer accumulation, same epilogue."""
+    from smpq import _lib, ops
+    g = torch.Generator().manual_seed(21 + limbs)
+    h, w = hw
+    wt = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(gpu)
+    x = torch.randn(2, 3, h, w, generator=g).to(gpu)
+    x[1] *= 5.0
+    am = ops.act_absmax(x)
+    lw = max(2, limbs)
+    codes4, _, wscale4, _ = ops.pack_weights_ex(wt, None, lw)
+    codes16, wscale16 = ops.pack_weights_s2d(wt, lw)
+    assert torch.equal(wscale4, wscale16)
+    cs = (wscale4 * torch.linspace(0.5, 2, 64, device=gpu)).contiguous()
+    sh = torch.linspace(-1, 1, 64, device=gpu).contiguous()
+    ya4 = torch.zeros(2, device=gpu)
+    y4 = ops.conv2d_q(ops.image_quantize(x, am, limbs), am, codes4, None, 7, 7, 2, 3, cs, sh, relu=True,
+                      y_absmax=ya4)
+    xs = ops.image_quantize_s2d(x, am, limbs)
+    rng = float(y4.abs().max()) * 1.5
+    ovf4 = torch.zeros(1, dtype=torch.int32, device=gpu)
+    _, yq4 = ops.conv2d_q(ops.image_quantize(x, am, limbs), am, codes4, None, 7, 7, 2, 3, cs, sh, relu=True,
+                          emit_range=rng, overflow=ovf4, want_f32=False)
+    tried = 0
+    for c in ops.tile_configs():
+        if ops.tile_kind(c) != ops.TILE_LDS_DMA:
+            continue
+        ya = torch.zeros(2, device=gpu)
+        try:
+            y = ops.stem_conv_s2d(xs, am, codes16, h, w, cs, sh, relu=True, y_absmax=ya, tile_cfg=c)
+        except _lib.SmpqError:
+            continue
+        tried += 1
+        assert torch.equal(y, y4), c
+        assert torch.equal(ya, ya4), c
+        ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+        _, yq = ops.stem_conv_s2d(xs, am, codes16, h, w, cs, sh, relu=True, tile_cfg=c, emit_range=rng,
+                                  overflow=ovf, want_f32=False)
+        assert torch.equal(yq, yq4), c
+        assert int(ovf.item()) == 0 == int(ovf4.item())
+    assert tried >= 3
+
+
+@pytest.mark.parametrize("limbs", [2, 3])
 def test_maxpool_quantize(gpu, limbs):
     from smpq import ops
     x = torch.relu(torch.randn(3, 17, 18, 64, generator=torch.Generator().manual_seed(2))).to(gpu)
