@@ -7,9 +7,17 @@ python bench.py --gpus N --steps K --warmup W       (N > 1: launched by torch.di
 
 One step = one fused forward of 256 synthetic 224x224 images per GPU (inputs generated on
 device, resident in HBM before the timed region) + the all-gather of the logits. Prints ONE
-JSON line on rank 0 with the roofline of the dominant kernel (qconv_kernel, timed with HIP
-events on its launch stream over the timed region) and the CPU baseline (the reference's
-fp32 torch-CPU forward restated in oracle/torch_ref.py, timed on a bounded sample).
+JSON line on rank 0 with the roofline of the dominant kernel family (the quantized conv:
+qconv_glds_kernel / qconv_kernel, every launch incl. the stem) and the CPU baseline (the
+reference's fp32 torch-CPU forward restated in oracle/torch_ref.py, timed on a bounded sample).
+
+Timing: `value` comes from the production path, the static-range forward replayed from a
+captured HIP graph. HIP events recorded inside a graph capture cannot be timed on ROCm 7.2
+(elapsed_time -> hipErrorInvalidHandle, tools/probe_graph_events.py), so the per-launch
+kernel durations come from a second region run right after the timed one: the same forward
+launched eagerly (the same kernels the graph replays) with HIP events around every conv
+launch on the stream it is launched on. The roofline is SURVEY.md 8(d)'s: per launch
+T_roof = max(2 MACs / P_int8, bytes / BW_HBM) with ops/ops.alg_work's algorithmic bytes.
 """
 import argparse
 import json
@@ -40,7 +48,7 @@ CONFIGS = {
 
 
 class ConvTimer:
-    """Events around every quantized-conv launch, on the stream it is launched on."""
+    """HIP events around every quantized-conv launch, on the stream it is launched on."""
 
     def __init__(self):
         self.recs = []
@@ -52,17 +60,48 @@ class ConvTimer:
             self._ev = torch.cuda.Event(enable_timing=True)
             self._ev.record(torch.cuda.current_stream())
 
-    def end(self, alg_ops, shape):
+    def end(self, work):
         if self.active:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(torch.cuda.current_stream())
-            self.recs.append((self._ev, e1, alg_ops, shape))
+            self.recs.append((self._ev, e1, work))
 
-    def summary(self):
+    def roofline(self, steps):
+        """per launch T_roof = max(ops / P_int8, bytes / BW); the reported
+        bound is the resource whose floor dominates the sum."""
         torch.cuda.synchronize()
-        total_ms = sum(a.elapsed_time(b) for a, b, _, _ in self.recs)
-        ops = sum(o for _, _, o, _ in self.recs)
-        return len(self.recs), total_ms, ops
+        t = [a.elapsed_time(b) * 1e-3 for a, b, _ in self.recs]
+        w = [r[2] for r in self.recs]
+        n = len(t)
+        t_sum = sum(t)
+        ops = sum(x["ops"] for x in w)
+        nbytes = sum(x["bytes"] for x in w)
+        pass_ops = sum(x["ops"] * x["passes"] for x in w)
+        t_mfma = ops / (INT8_DENSE_PEAK_TOPS * 1e12)
+        t_hbm = nbytes / (HBM_PEAK_GBS * 1e9)
+        t_roof = sum(max(x["ops"] / (INT8_DENSE_PEAK_TOPS * 1e12), x["bytes"] / (HBM_PEAK_GBS * 1e9)) for x in w)
+        hbm_gbs = nbytes / t_sum / 1e9
+        tops = ops / t_sum / 1e12
+        if t_hbm >= t_mfma:
+            bound, achieved, peak, unit = "hbm", hbm_gbs, HBM_PEAK_GBS, "GB/s"
+        else:
+            bound, achieved, peak, unit = "mfma", tops, INT8_DENSE_PEAK_TOPS, "TFLOP/s"
+        return {
+            "bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": None,
+            "kernel": "quantized conv (qconv_glds_kernel + qconv_kernel), all launches incl. the stem",
+            "launches_per_step": n // max(steps, 1),
+            "avg_launch_ms": round(t_sum / max(n, 1) * 1e3, 5),
+            "alg_bytes_per_launch": round(nbytes / max(n, 1)),
+            "alg_ops_per_launch": round(ops / max(n, 1)),
+            "t_roof_over_t": round(t_roof / t_sum, 4),
+            "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 4),
+            "mfma_frac": round(tops / INT8_DENSE_PEAK_TOPS, 4),
+            "mfma_frac_incl_limb_passes": round(pass_ops / t_sum / 1e12 / INT8_DENSE_PEAK_TOPS, 4),
+            "conv_ms_per_step": round(t_sum / max(steps, 1) * 1e3, 4),
+            "timing": "HIP events per launch over %d eager steps right after the graph-replayed timed "
+                      "region (same kernels; events cannot time inside a replayed HIP graph)" % steps,
+        }
 
 
 def cpu_baseline(arch, assign_name, budget_s=12.0):
@@ -103,7 +142,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
     ap.add_argument("--config", default="r50_mixed", choices=sorted(CONFIGS))
-    ap.add_argument("--limbs", type=int, default=2, help="activation int8 limbs (2 = int16)")
+    ap.add_argument("--limbs", type=int, default=3,
+                    help="activation int8 limbs: 3 = int24 codes (parity mode, default), 2 = int16 (fast mode)")
+    ap.add_argument("--roofline-steps", type=int, default=3, help="eager steps timed per launch for the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--chunk", type=int, default=None, help="images per pass (Infinity-Cache blocking)")
@@ -151,20 +192,15 @@ def main():
     if rank == 0:
         print("autotuned tiles:", {"x".join(map(str, k[:8])): v for k, v in ops._TUNED.items()},
               file=sys.stderr, flush=True)
-    timer = ConvTimer()
-    ops.set_conv_hook(timer)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    timer.active = True
-    h0 = stats["hip_conv"]
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    timer.active = False
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
@@ -172,15 +208,25 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    hip_convs = stats["hip_conv"] - h0
-    n_launch, kern_ms, alg_ops = timer.summary()
+
+    # per-launch kernel times for the roofline: the same forward, launched eagerly
+    timer = ConvTimer()
+    use_graph = engine.USE_GRAPH[0]
+    engine.USE_GRAPH[0] = False
+    ops.set_conv_hook(timer)
+    step()  # untimed: the eager path's first pass
+    timer.active = True
+    for _ in range(args.roofline_steps):
+        step()
+    timer.active = False
     ops.set_conv_hook(None)
+    engine.USE_GRAPH[0] = use_graph
+    roof = timer.roofline(args.roofline_steps)
 
     images = args.batch * world * args.steps
     value = images / elapsed
-    per_launch_ops = alg_ops / max(n_launch, 1)
-    avg_ms = kern_ms / max(n_launch, 1)
-    achieved_tops = per_launch_ops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    ms_per_step = elapsed / args.steps * 1e3
+    roof["kernel_share_of_step"] = round(roof["conv_ms_per_step"] / ms_per_step, 4)
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -189,7 +235,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -198,14 +244,10 @@ def main():
             "config": {"workload": desc, "assignment": assign, "batch_per_gpu": args.batch,
                        "global_batch": args.batch * world, "act_limbs": args.limbs,
                        "act_code": {1: "int8", 2: "int16 (2 int8 limbs)", 3: "int24 (3 int8 limbs)"}[args.limbs],
-                       "parallelism": "dp%d" % world, "quantized_convs_per_step": hip_convs // max(args.steps, 1),
-                       "range_mode": engine.get_range_mode(), "chunk": engine.CHUNK[0]},
-            "roofline": {"bound": "mfma", "kernel": "qconv_kernel", "achieved": round(achieved_tops, 2),
-                         "peak": INT8_DENSE_PEAK_TOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved_tops / INT8_DENSE_PEAK_TOPS, 4), "traffic": None,
-                         "alg_ops_per_launch": per_launch_ops, "avg_launch_ms": round(avg_ms, 5),
-                         "launches": n_launch, "mfma_passes_per_alg_op": args.limbs,
-                         "kernel_share_of_step": round(kern_ms / (elapsed * 1e3), 4)},
+                       "parallelism": "dp%d" % world, "quantized_convs_per_step": roof["launches_per_step"],
+                       "range_mode": engine.get_range_mode(), "chunk": engine.CHUNK[0],
+                       "hip_graph": bool(engine.USE_GRAPH[0])},
+            "roofline": roof,
         }
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(arch, assign, args.cpu_budget)

@@ -10,8 +10,11 @@ import torch
 from . import _lib
 
 # activation code width in int8 limbs (1 = int8, 2 = int16, 3 = int24); see DESIGN.md
-_ACT_LIMBS = [2]
-# optional launch observer (bench.py): object with begin() / end(alg_ops, shape) around each conv
+# Activation code width in int8 limbs: 3 (int24, the default) is the parity mode — logits within
+# 2e-4 relative of the fp32 reference and identical top-1 labels; 2 (int16) is the fast mode
+# (~1e-2 relative logit error, top-1 identical except at near-ties); 1 (int8) is for experiments.
+_ACT_LIMBS = [int(os.environ.get("SMPQ_ACT_LIMBS", "3"))]
+# optional launch observer (bench.py): object with begin() / end(work) around each conv
 _CONV_HOOK = [None]
 LIMB_QMAX = {1: 127.0, 2: 32512.0, 3: 8323072.0}
 
@@ -175,11 +178,16 @@ def stem_conv_s2d(xq, x_absmax, codes, h, w, col_scale, col_shift, relu=True, y_
         _req(overflow is not None, "stem_conv_s2d: emit_range needs an overflow flag tensor")
         yq = torch.empty(limbs, n, ho, wo, cout, dtype=torch.int8, device=xq.device)
     lib = _lib.load()
+    hook = _CONV_HOOK[0]
+    if hook is not None:
+        hook.begin()
     with torch.cuda.device(xq.device):
         _lib.check(lib.smpq_stem_conv_s2d_q(
             _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, _lib.ptr(codes), int(wlimbs), cout, _lib.ptr(col_scale),
             _lib.ptr(col_shift), 1 if relu else 0, int(limbs), _lib.ptr(y), _lib.ptr(y_absmax), _lib.ptr(yq),
             float(emit_range or 0.0), _lib.ptr(overflow), int(tile_cfg), _lib.stream_ptr()), "smpq_stem_conv_s2d_q")
+    if hook is not None:
+        hook.end(alg_work(n, h, w, 3, cout, 7, 7, ho, wo, limbs, wlimbs, y is not None, yq is not None, False, False))
     return y if emit_range is None else (y, yq)
 
 
@@ -356,7 +364,9 @@ def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_sh
             _lib.ptr(overflow), _lib.ptr(residual_q), float(residual_range or 0.0), int(tile_cfg),
             _lib.stream_ptr()), "smpq_conv2d_fwd_q")
     if hook is not None:
-        hook.end(2 * n * ho * wo * cout * kh * kw * min(cin, 3 if cin == 4 else cin), (n, h, w, cin, cout, kh, stride))
+        cin_real = 3 if cin == 4 else cin  # the 4-channel stem planes carry RGB + a zero channel
+        hook.end(alg_work(n, h, w, cin_real, cout, kh, kw, ho, wo, limbs, wlimbs, out is not None, yq is not None,
+                          residual is not None, residual_q is not None))
     if emit_range is not None:
         return out, yq
     return out
@@ -433,7 +443,27 @@ def conv2d_nhwc(x, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_
 
 
 def set_conv_hook(hook):
+    """hook.begin() / hook.end(work) around every quantized-conv launch (bench.py's timer);
+    work = alg_work(...) of the launch."""
     _CONV_HOOK[0] = hook
+
+
+def alg_work(n, h, w, cin, cout, kh, kw, ho, wo, limbs, wlimbs, y_f32, y_q, res_f32, res_q):
+    """Algorithmic work of one quantized-conv launch: ops = 2 * MACs; bytes =
+    each input activation code read once (limbs bytes per element: the int8/16/24 code), the
+    weight codes once, and every output element written once (limbs bytes for the next conv's
+    limb planes, 4 for fp32) plus its residual read once (limbs or 4 bytes). Halo re-reads of
+    3x3 windows and zero padding are not counted: they are the kernel's overhead."""
+    macs = n * ho * wo * cout * kh * kw * cin
+    out_elems = n * ho * wo * cout
+    per_out = (4 if y_f32 else 0) + (limbs if y_q else 0) + (4 if res_f32 else 0) + (limbs if res_q else 0)
+    nbytes = limbs * n * h * w * cin + wlimbs * cout * kh * kw * cin + out_elems * per_out
+    return {"ops": 2 * macs, "bytes": nbytes, "passes": limbs * wlimbs - _skipped_passes(limbs, wlimbs)}
+
+
+def _skipped_passes(limbs, wlimbs):
+    smin = max(0, limbs + wlimbs - 4)  # low-digit products skipped by the kernels (conv.hip)
+    return sum(1 for la in range(limbs) for lw in range(wlimbs) if la + lw < smin)
 
 
 def debug_mfma_i8(a, b):
