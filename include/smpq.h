@@ -162,6 +162,11 @@ int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int
                       int8_t* yq, float yq_range, int32_t* overflow, const int8_t* residual_q,
                       float residual_range, int tile_cfg, smpq_stream_t stream);
 
+/* 3x3 / stride 2 / pad 1 max pool (resnet.py:147) directly on int8 limb planes
+ * x [limbs][n][h][w][c] -> out [limbs][n][ho][wo][c], c % 16 == 0 (static-range mode: the codes of
+ * one activation share one step, so the max of the codes is the code of the max — exact). */
+int smpq_maxpool_limbs(const int8_t* x, int n, int h, int w, int c, int limbs, int8_t* out, smpq_stream_t stream);
+
 /* ---- space-to-depth stem (the 7x7 / stride 2 / pad 3 conv1 of resnet.py:143) -------------------
  * The stem runs as a 4x4 / stride 1 conv over 16-channel "space-to-depth" pixels (each a 2x2
  * block of the image with up to 4 channels), so every 64-byte K step of the int8 GEMM is one

@@ -30,6 +30,7 @@
 // k; one LDS double buffer, one barrier per K step; the epilogue reuses the LDS arena as an fp32
 // output tile so residual loads and output stores are whole 16-B pieces of contiguous rows.
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 #include <string>
 
@@ -680,6 +681,60 @@ __global__ __launch_bounds__(256) void maxpool_quantize_kernel(const float* __re
   }
 }
 
+// 3x3 / stride 2 / pad 1 max pool on int8 limb planes [L][n][h][w][c] (c % 16 == 0): the codes of
+// one activation share one step, so the max of the codes is the code of the max (the quantizer
+// is monotone) — exact. One thread = 16 channels of one output pixel (16-B loads per limb).
+template <int L>
+__global__ __launch_bounds__(256) void maxpool_limbs_kernel(const int8_t* __restrict__ x, int n, int h, int w, int c,
+                                                            int ho, int wo, long long iplane,
+                                                            int8_t* __restrict__ out, long long oplane) {
+  const int c16 = c / 16;
+  const long long total = (long long)n * ho * wo * c16;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int cq = (int)(t % c16);
+    long long p = t / c16;
+    const int ow = (int)(p % wo);
+    p /= wo;
+    const int oh = (int)(p % ho);
+    const int img = (int)(p / ho);
+    int m[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m[k] = INT_MIN;
+    for (int dr = 0; dr < 3; ++dr) {
+      const int ih = 2 * oh - 1 + dr;
+      if ((unsigned)ih >= (unsigned)h) continue;
+      for (int dc = 0; dc < 3; ++dc) {
+        const int iw = 2 * ow - 1 + dc;
+        if ((unsigned)iw >= (unsigned)w) continue;
+        const size_t off = (((size_t)img * h + ih) * w + iw) * c + 16 * cq;
+        v4i d[L];
+#pragma unroll
+        for (int l = 0; l < L; ++l) d[l] = *reinterpret_cast<const v4i*>(x + l * iplane + off);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          int q = 0;
+#pragma unroll
+          for (int l = L - 1; l >= 0; --l) q = q * 256 + (int)(int8_t)((unsigned)d[l][k >> 2] >> (8 * (k & 3)));
+          m[k] = max(m[k], q);
+        }
+      }
+    }
+    const size_t o = (((size_t)img * ho + oh) * wo + ow) * c + 16 * cq;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      unsigned wd[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        int dg[L];
+        split_limbs<L>(m[k], dg);
+        wd[k >> 2] |= (unsigned)(dg[l] & 255) << (8 * (k & 3));
+      }
+      *reinterpret_cast<v4i*>(out + l * oplane + o) = v4i{(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, int64_t per_image,
                                                      float* __restrict__ out) {
   const int img = blockIdx.y;
@@ -1063,6 +1118,24 @@ extern "C" int smpq_maxpool_quantize(const float* x, int n, int h, int w, int c,
     default: return fail(SMPQ_E_INVALID, "smpq_maxpool_quantize: limbs must be 1, 2 or 3");
   }
   return check_hip(hipGetLastError(), "maxpool_quantize_kernel launch");
+}
+
+extern "C" int smpq_maxpool_limbs(const int8_t* x, int n, int h, int w, int c, int limbs, int8_t* out,
+                                  smpq_stream_t stream) {
+  if (!x || !out || n <= 0 || h <= 0 || w <= 0 || c <= 0 || (c % 16) != 0)
+    return fail(SMPQ_E_INVALID, "smpq_maxpool_limbs: bad arguments (c % 16 == 0)");
+  const int ho = (h + 2 - 3) / 2 + 1, wo = (w + 2 - 3) / 2 + 1;
+  const long long iplane = (long long)n * h * w * c, oplane = (long long)n * ho * wo * c;
+  const long long total = (long long)n * ho * wo * (c / 16);
+  const dim3 grid((unsigned)std::min<long long>((total + 255) / 256, 65535));
+  hipStream_t s = (hipStream_t)stream;
+  switch (limbs) {
+    case 1: hipLaunchKernelGGL(maxpool_limbs_kernel<1>, grid, dim3(256), 0, s, x, n, h, w, c, ho, wo, iplane, out, oplane); break;
+    case 2: hipLaunchKernelGGL(maxpool_limbs_kernel<2>, grid, dim3(256), 0, s, x, n, h, w, c, ho, wo, iplane, out, oplane); break;
+    case 3: hipLaunchKernelGGL(maxpool_limbs_kernel<3>, grid, dim3(256), 0, s, x, n, h, w, c, ho, wo, iplane, out, oplane); break;
+    default: return fail(SMPQ_E_INVALID, "smpq_maxpool_limbs: limbs must be 1, 2 or 3");
+  }
+  return check_hip(hipGetLastError(), "maxpool_limbs_kernel launch");
 }
 
 extern "C" int smpq_act_absmax(const float* x, int n, int64_t per_image, float* absmax,

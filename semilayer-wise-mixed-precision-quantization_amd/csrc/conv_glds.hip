@@ -111,7 +111,20 @@ __device__ __forceinline__ unsigned pack_bytes(int b0, int b1, int b2, int b3, i
 // S2D: the space-to-depth stem. The image is stored as 16-channel pixels ([2x2 block][4 ch]) and
 // the 7x7/2 conv is a 4x4/1 conv over them (pad 2, zero taps where the 8x8 extension falls
 // outside 7x7); a 64-B K step is one tap row: lane chunk c = the 16 channels of tap column c.
-template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D>
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+#define SMPQ_VMW(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    SMPQ_VMW(1) SMPQ_VMW(2) SMPQ_VMW(3) SMPQ_VMW(4) SMPQ_VMW(5) SMPQ_VMW(6) SMPQ_VMW(7) SMPQ_VMW(8)
+    SMPQ_VMW(9) SMPQ_VMW(10) SMPQ_VMW(11) SMPQ_VMW(12) SMPQ_VMW(13) SMPQ_VMW(14) SMPQ_VMW(15) SMPQ_VMW(16)
+#undef SMPQ_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// NST LDS stages: the DMA of K step k + NST - 1 is in flight while step k computes.
+template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST>
 __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kernel(ConvArgs a) {
   constexpr int NW = WAVES_C * WAVES_P;
   constexpr int BC = 16 * WC * WAVES_C;  // channels per block tile
@@ -124,7 +137,7 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
   constexpr int STAGE = NPIECE * 1024;
   constexpr int WSLOTS = (WPIECES + NW - 1) / NW;
   constexpr int ASLOTS = (APIECES + NW - 1) / NW;
-  extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // 1 stage (ksteps == 1) or 2
+  extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // min(NST, ksteps) stages
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -298,14 +311,48 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
                                                                                   (unsigned)((long long)l * oplane), 0);
   }
 
-  int kr = 0, kc = 0, c0 = 0;
-  issue(0, 0, 0, 0, 0);
+  // DMA pieces this wave issues per K step (wave-uniform): the counted vmcnt below
+  int ppw = 0;
+#pragma unroll
+  for (int s = 0; s < WSLOTS; ++s) ppw += (wave + NW * s < WPIECES) ? 1 : 0;
+#pragma unroll
+  for (int s = 0; s < ASLOTS; ++s) ppw += (wave + NW * s < APIECES) ? 1 : 0;
+
+  int kr = 0, kc = 0, c0 = 0;  // K position of the next step to issue
+  auto advance = [&]() {
+    c0 += kKStep;
+    if (c0 == a.cin) {
+      c0 = 0;
+      if (++kc == a.kw) {
+        kc = 0;
+        ++kr;
+      }
+    }
+  };
+  int nissued = 0, wbuf = 0, rbuf = 0;
+#pragma unroll
+  for (int st = 0; st < NST - 1; ++st) {
+    if (st < a.ksteps) {
+      issue(wbuf, kr, kc, c0, st);
+      advance();
+      ++nissued;
+      wbuf = wbuf + 1 == NST ? 0 : wbuf + 1;
+    }
+  }
   for (int ks = 0; ks < a.ksteps; ++ks) {
-    const int buf = ks & 1;
-    // this wave's DMA of step ks has landed and its reads of step ks-1 are done; after the
-    // barrier every wave's are, so stage ks is readable and stage ks-1 may be refilled
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const int8_t* sb = lds + buf * STAGE;
+    // this wave's DMA of step ks has landed (the younger steps' may still fly) and its reads of
+    // step ks-1 are done; after the barrier every wave's are, so stage ks is readable and the
+    // stage of step ks-1 may be refilled
+    if constexpr (NST == 2) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    } else {
+      wait_vmcnt((nissued - ks - 1) * ppw);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int8_t* sb = lds + rbuf * STAGE;
+    rbuf = rbuf + 1 == NST ? 0 : rbuf + 1;
     v4i wf[LW][WC], af[L][WP];
 #pragma unroll
     for (int lw = 0; lw < LW; ++lw)
@@ -317,16 +364,13 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 #pragma unroll
       for (int j = 0; j < WP; ++j)
         af[l][j] = *reinterpret_cast<const v4i*>(sb + (WPIECES + l * (BP / 16) + wp * WP + j) * 1024 + rd);
-    // advance the K position and start the next step's DMA into the other stage
-    c0 += kKStep;
-    if (c0 == a.cin) {
-      c0 = 0;
-      if (++kc == a.kw) {
-        kc = 0;
-        ++kr;
-      }
+    // start the DMA of step ks + NST - 1 into the stage step ks - 1 used
+    if (nissued < a.ksteps) {
+      issue(wbuf, kr, kc, c0, nissued);
+      advance();
+      ++nissued;
+      wbuf = wbuf + 1 == NST ? 0 : wbuf + 1;
     }
-    if (ks + 1 < a.ksteps) issue(buf ^ 1, kr, kc, c0, ks + 1);
     if (do_off) {
 #pragma unroll
       for (int l = 0; l < L; ++l)
@@ -547,19 +591,28 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 
 // ------------------------------------------------------------------------------------------
 struct GldsCfg {
-  int wavesc, wavesp, wc, wp;
+  int wavesc, wavesp, wc, wp, stages;
 };
 constexpr GldsCfg kGlds[] = {
-    {2, 2, 2, 2},  // 0:  64 ch x  64 px, 256 threads
-    {2, 2, 2, 4},  // 1:  64 ch x 128 px
-    {2, 2, 4, 2},  // 2: 128 ch x  64 px
-    {1, 4, 4, 1},  // 3:  64 ch x  64 px (each wave all 64 channels of 16 px)
-    {1, 4, 4, 2},  // 4:  64 ch x 128 px
-    {4, 1, 2, 4},  // 5: 128 ch x  64 px (each wave 32 ch x all 64 px)
-    {2, 2, 4, 4},  // 6: 128 ch x 128 px (<= 2 accumulator sets)
-    {4, 1, 4, 2},  // 7: 256 ch x  32 px (whole 256-B output rows per block: wide 1x1 expansions)
-    {4, 1, 4, 1},  // 8: 256 ch x  16 px
-    {2, 2, 4, 1},  // 9: 128 ch x  32 px
+    {2, 2, 2, 2, 2},  // 0:  64 ch x  64 px, 256 threads
+    {2, 2, 2, 4, 2},  // 1:  64 ch x 128 px
+    {2, 2, 4, 2, 2},  // 2: 128 ch x  64 px
+    {1, 4, 4, 1, 2},  // 3:  64 ch x  64 px (each wave all 64 channels of 16 px)
+    {1, 4, 4, 2, 2},  // 4:  64 ch x 128 px
+    {4, 1, 2, 4, 2},  // 5: 128 ch x  64 px (each wave 32 ch x all 64 px)
+    {2, 2, 4, 4, 2},  // 6: 128 ch x 128 px (<= 2 accumulator sets)
+    {4, 1, 4, 2, 2},  // 7: 256 ch x  32 px (whole 256-B output rows per block: wide 1x1 expansions)
+    {4, 1, 4, 1, 2},  // 8: 256 ch x  16 px
+    {2, 2, 4, 1, 2},  // 9: 128 ch x  32 px
+    {2, 2, 2, 2, 3},  // 10: as 0, 3 LDS stages (DMA two K steps ahead; long-K 3x3 convs)
+    {1, 4, 4, 1, 3},  // 11: as 3, 3 stages
+    {2, 2, 4, 2, 3},  // 12: as 2, 3 stages
+    // 8 waves: twice the MFMA work per loaded byte (the 3x3 convs stream ~100 ops/B from L2 at 64 x 64)
+    {2, 4, 4, 2, 2},  // 13: 128 ch x 128 px (waves 64 ch x 32 px)
+    {4, 2, 2, 4, 2},  // 14: 128 ch x 128 px (waves 32 ch x 64 px)
+    {1, 8, 4, 2, 2},  // 15:  64 ch x 256 px
+    {2, 4, 2, 4, 2},  // 16:  64 ch x 256 px (waves 32 ch x 64 px)
+    {4, 2, 4, 2, 2},  // 17: 256 ch x  64 px
 };
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
@@ -572,7 +625,7 @@ void glds_cfg_info(int cfg, int* bm, int* bn, int* threads) {
   *threads = 64 * c.wavesc * c.wavesp;
 }
 
-template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, bool S2D = false>
+template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, bool S2D = false, int NST = 2, int MINW = 2>
 static int launch_one(const ConvArgs& a, hipStream_t stream) {
   constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
   if constexpr ((L + LW - 1 - SMIN) * WC * WP * 4 > 128) {
@@ -583,12 +636,12 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
     const long nt = (a.cout + BC - 1) / BC;
     if (mt * nt > 0x7fffffffL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
     constexpr int STAGE = (LW * (BC / 16) + L * (BP / 16)) * 1024;
-    auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, 2, S2D>;
+    auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST>;
     static const hipError_t attr =
-        hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 2 * STAGE);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, NST * STAGE);
     if (attr != hipSuccess) return check_hip(attr, "qconv_glds_kernel LDS attribute");
-    // a single K step needs one LDS stage: twice the blocks per CU for the 1x1 convs with cin 64
-    const int lds_bytes = (a.ksteps > 1 ? 2 : 1) * STAGE;
+    // no more stages than K steps: a single-step conv (1x1, cin 64) needs one
+    const int lds_bytes = (a.ksteps < NST ? a.ksteps : NST) * STAGE;
     hipLaunchKernelGGL(kern, dim3((unsigned)(mt * nt)), dim3(64 * WAVES_C * WAVES_P), lds_bytes, stream, a);
     return check_hip(hipGetLastError(), "qconv_glds_kernel launch");
   }
@@ -607,6 +660,14 @@ static int launch_cfg(int cfg, const ConvArgs& a, hipStream_t s) {
     case 7: return launch_one<L, LW, 4, 1, 4, 2>(a, s);
     case 8: return launch_one<L, LW, 4, 1, 4, 1>(a, s);
     case 9: return launch_one<L, LW, 2, 2, 4, 1>(a, s);
+    case 10: return launch_one<L, LW, 2, 2, 2, 2, false, 3>(a, s);
+    case 11: return launch_one<L, LW, 1, 4, 4, 1, false, 3>(a, s);
+    case 12: return launch_one<L, LW, 2, 2, 4, 2, false, 3>(a, s);
+    case 13: return launch_one<L, LW, 2, 4, 4, 2>(a, s);
+    case 14: return launch_one<L, LW, 4, 2, 2, 4>(a, s);
+    case 15: return launch_one<L, LW, 1, 8, 4, 2>(a, s);
+    case 16: return launch_one<L, LW, 2, 4, 2, 4>(a, s);
+    case 17: return launch_one<L, LW, 4, 2, 4, 2>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   }
 }

@@ -49,6 +49,7 @@ _PROTOS = {
                              _vp, _i, _i, _vp, _vp, _i, _vp]),
     "smpq_conv2d_fwd_q": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp,
                                _vp, _i, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, ctypes.c_float, _i, _vp]),
+    "smpq_maxpool_limbs": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "smpq_image_quantize_s2d": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
     "smpq_pack_weights_s2d": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
     "smpq_stem_conv_s2d_q": (_i, [_vp, _vp, _i, _i, _i, _vp, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp,

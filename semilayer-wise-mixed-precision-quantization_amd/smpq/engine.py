@@ -203,7 +203,9 @@ def block_forward(blk, x, ctx=None, last=False):
     activation is stored in fp32 except the downsample's identity and the last block's output
     (avgpool): the identity of a block without downsample is read from its input's limb planes."""
     if blk.downsample is not None:
-        identity = run_conv(blk.downsample[0], blk.downsample[1], x, relu=False, want_amax=False, ctx=ctx).f32
+        # static mode: the identity as calibrated-range limb planes (3 B/element instead of fp32)
+        ds = run_conv(blk.downsample[0], blk.downsample[1], x, relu=False, ctx=ctx, want_f32=False)
+        identity = ds if (ds.f32 is None and ds.q is not None and ds.rng is not None) else ds.f32
     elif x.f32 is not None or x.q is None or x.rng is None:
         identity = x.f32
     else:
@@ -246,8 +248,10 @@ def stem_s2d_plan(conv, bn):
     return plan
 
 
-def stem_forward(model, x):
-    """conv1 7x7/2 + bn1 + relu + maxpool 3x3/2 (resnet.py:206-209) -> Act of the pooled output."""
+def stem_forward(model, x, ctx=None):
+    """conv1 7x7/2 + bn1 + relu + maxpool 3x3/2 (resnet.py:206-209) -> Act of the pooled output.
+    Static-range mode: the stem writes its calibrated-range limb planes and the max pool works on
+    the codes (exact: the quantizer is monotone); no fp32 tensor is written."""
     x = x.float().contiguous()
     n = x.shape[0]
     pool_ok = isinstance(model.maxpool, torch.nn.MaxPool2d) and model.maxpool.kernel_size in (3, (3, 3)) \
@@ -259,12 +263,22 @@ def stem_forward(model, x):
         codes, col_scale, col_shift = s2d
         amax_in = ops.act_absmax(x)
         xq = ops.image_quantize_s2d(x, amax_in)
-        yam = torch.zeros(n, dtype=torch.float32, device=x.device)
-        y = ops.tuned_stem_conv_s2d(xq, amax_in, codes, x.shape[2], x.shape[3], col_scale, col_shift,
-                                    relu=True, y_absmax=yam)
         stats["hip_conv"] += 1
         stats["fixed_conv"] += 1
         model.conv1.last_path = "hip-fixed-s2d"
+        conv = model.conv1
+        if ctx is not None and ctx.ranges is not None and id(conv) in ctx.ranges and conv.out_channels % 16 == 0:
+            rng = ctx.ranges[id(conv)]
+            _, yq = ops.tuned_stem_conv_s2d(xq, amax_in, codes, x.shape[2], x.shape[3], col_scale, col_shift,
+                                            relu=True, emit_range=rng, overflow=ctx.overflow, want_f32=False)
+            return Act(q=ops.maxpool_limbs(yq), amax=ctx.range_tensor(conv), rng=rng)
+        yam = torch.zeros(n, dtype=torch.float32, device=x.device)
+        y = ops.tuned_stem_conv_s2d(xq, amax_in, codes, x.shape[2], x.shape[3], col_scale, col_shift,
+                                    relu=True, y_absmax=yam)
+        if ctx is not None and ctx.record is not None:
+            prev = ctx.record.get(id(conv))
+            m = yam.amax().reshape(1)
+            ctx.record[id(conv)] = m if prev is None else torch.maximum(prev, m)
         q, f = ops.maxpool_quantize(y, yam, want_f32=True)
         return Act(f32=f, q=q, amax=yam)
     plan = conv_plan(model.conv1, model.bn1)
@@ -285,7 +299,7 @@ def _blocks(model):
 
 
 def _features(model, x, ctx):
-    act = stem_forward(model, x)
+    act = stem_forward(model, x, ctx)
     blocks = _blocks(model)
     for i, blk in enumerate(blocks):
         act = block_forward(blk, act, ctx, last=(i == len(blocks) - 1))

@@ -221,6 +221,20 @@ def tuned_stem_conv_s2d(xq, x_absmax, codes, h, w, col_scale, col_shift, relu=Tr
                          -1 if cfg is None else cfg, **kw)
 
 
+def maxpool_limbs(xq):
+    """3x3/2/1 max pool on limb planes [L, n, h, w, c] (c % 16 == 0) -> [L, n, ho, wo, c] (exact:
+    the quantizer is monotone, so pooling the codes = quantizing the pooled values)."""
+    limbs, n, h, w, c = xq.shape
+    _req(xq.is_cuda and xq.dtype == torch.int8 and xq.is_contiguous() and c % 16 == 0, "maxpool_limbs: planes")
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    out = torch.empty(limbs, n, ho, wo, c, dtype=torch.int8, device=xq.device)
+    lib = _lib.load()
+    with torch.cuda.device(xq.device):
+        _lib.check(lib.smpq_maxpool_limbs(_lib.ptr(xq), n, h, w, c, int(limbs), _lib.ptr(out), _lib.stream_ptr()),
+                   "smpq_maxpool_limbs")
+    return out
+
+
 def maxpool_quantize(x_nhwc, x_absmax, limbs=None, want_f32=True):
     """MaxPool2d(3, 2, 1) on NHWC fp32 fused with the activation quantizer of its output.
     Returns (limb planes [limbs, n, ho, wo, c], fp32 NHWC pooled or None)."""

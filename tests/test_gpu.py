@@ -604,6 +604,19 @@ def test_stem_s2d_bitwise_matches_4ch_stem(gpu, limbs, hw):
     assert tried >= 3
 
 
+@pytest.mark.parametrize("limbs", [1, 2, 3])
+def test_maxpool_limbs_equals_quantized_maxpool(gpu, limbs):
+    """Max pool on the codes == the codes of the max pool (monotone quantizer), bit for bit."""
+    import torch.nn.functional as F
+    from smpq import ops
+    g = torch.Generator().manual_seed(5 + limbs)
+    x = torch.relu(torch.randn(3, 17, 22, 32, generator=g)).to(gpu)  # NHWC, odd/even sizes
+    rng = torch.full((3,), float(x.abs().max()) * 1.3, device=gpu)
+    xq = ops.act_quantize(x, rng, limbs)
+    pooled = F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1).contiguous()
+    assert torch.equal(ops.maxpool_limbs(xq), ops.act_quantize(pooled, rng, limbs))
+
+
 @pytest.mark.parametrize("limbs", [2, 3])
 def test_maxpool_quantize(gpu, limbs):
     from smpq import ops
