@@ -203,11 +203,18 @@ int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads);
  *   SMPQ_TILE_REGSTAGE_SMALLC  register-staged loader, also cin == 4 (the stem)
  *   SMPQ_TILE_LDS_DMA          LDS-DMA loader; cin % 64 == 0, cout % 16 == 0, every operand and
  *                              output plane < 2 GiB
+ *   SMPQ_TILE_LDS_DMA_K128     as SMPQ_TILE_LDS_DMA with 128-wide K steps: also cin % 128 == 0
  * (negative: error code). */
 #define SMPQ_TILE_REGSTAGE 0
 #define SMPQ_TILE_REGSTAGE_SMALLC 1
 #define SMPQ_TILE_LDS_DMA 2
+#define SMPQ_TILE_LDS_DMA_K128 3
 int smpq_conv2d_tile_kind(int cfg);
+
+/* 1 if tile configuration cfg can run a conv of this shape and these limb counts (the rules the
+ * launch applies: loader family, K-step width, accumulator budget, LDS per CU), else 0. Every
+ * supported configuration gives bitwise-identical results. */
+int smpq_conv2d_tile_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs);
 
 /* Workspace the conv needs (none today; kept for ABI stability). */
 size_t smpq_conv2d_workspace_bytes(int n, int h, int w, int cin, int cout, int kh, int kw,

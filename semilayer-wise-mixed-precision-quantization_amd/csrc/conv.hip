@@ -970,10 +970,26 @@ extern "C" int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, i
 
 extern "C" int smpq_conv2d_num_tile_configs(void) { return kNumTileCfgs + glds_num_cfgs(); }
 
+extern "C" int smpq_conv2d_tile_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs) {
+  if (cfg < 0 || cfg >= kNumTileCfgs + glds_num_cfgs() || limbs < 1 || limbs > 3 || wlimbs < 1 || wlimbs > 3)
+    return 0;
+  if (cfg >= kNumTileCfgs) return glds_supported(cfg - kNumTileCfgs, cin, cout, kh, kw, limbs, wlimbs) ? 1 : 0;
+  const TileCfg& t = kTileCfgs[cfg % kNumBaseCfgs];
+  const int b = cfg % kNumBaseCfgs;
+  if (cin == 4) {
+    if (!(b == 2 || b == 3) || wlimbs < 2 || limbs < 2) return 0;
+  } else if (cin % kKStep != 0) {
+    return 0;
+  }
+  if (wlimbs == 3 && limbs != 3) return 0;
+  const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
+  return (limbs + wlimbs - 1 - smin) * t.wm * t.wn * 4 <= 128 ? 1 : 0;
+}
+
 extern "C" int smpq_conv2d_tile_kind(int cfg) {
   if (cfg < 0 || cfg >= kNumTileCfgs + glds_num_cfgs())
     return fail(SMPQ_E_INVALID, "smpq_conv2d_tile_kind: bad config");
-  if (cfg >= kNumTileCfgs) return SMPQ_TILE_LDS_DMA;
+  if (cfg >= kNumTileCfgs) return glds_cfg_bk(cfg - kNumTileCfgs) == 128 ? SMPQ_TILE_LDS_DMA_K128 : SMPQ_TILE_LDS_DMA;
   const int b = cfg % kNumBaseCfgs;
   return (b == 2 || b == 3) ? SMPQ_TILE_REGSTAGE_SMALLC : SMPQ_TILE_REGSTAGE;
 }

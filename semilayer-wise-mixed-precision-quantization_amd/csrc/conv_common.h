@@ -59,6 +59,8 @@ __device__ __forceinline__ float affine(float v, float rscale, float cscale, flo
 // LDS-DMA staged kernel (conv_glds.hip)
 int glds_num_cfgs();
 void glds_cfg_info(int cfg, int* bm, int* bn, int* threads);
+int glds_cfg_bk(int cfg);
+bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs);
 int launch_glds(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s);
 
 }  // namespace smpq

@@ -67,7 +67,14 @@ __device__ __forceinline__ void dma16(unsigned lds, v4i rsrc, unsigned voff, uns
       : "memory");
 }
 
-__device__ __forceinline__ int swz(int row) { return (4 - (row >> 2)) & 3; }
+// LDS image of a [rows][BK] operand region: the 16-B chunk c of row r is stored at c ^ swz<BK>(r).
+// Conflict-free for the DMA's lane-linear writes and for ds_read_b128 fragment reads (16 rows,
+// 16 B each, gfx950 b128 lane groups): BK = 64 rows are 4 chunks, BK = 128 rows are 8 chunks.
+template <int BK>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (BK == 64) return (4 - (row >> 2)) & 3;
+  else return (row >> 1) & 7;
+}
 
 // 4 x 4 transpose of (lane group g = lane >> 4, register c): afterwards group g register c holds
 // what group c register g held. v_permlane32_swap exchanges the upper half of its first operand
@@ -124,15 +131,22 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 }
 
 // NST LDS stages: the DMA of K step k + NST - 1 is in flight while step k computes.
-template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST>
+// BK: K bytes per stage and row. 64 = one MFMA K; 128 (cin % 128 == 0) = two, and every DMA piece
+// is then 8 whole 128-B lines instead of 16 half lines (half the TA/TD work per byte).
+template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK>
 __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kernel(ConvArgs a) {
+  static_assert(BK == 64 || BK == 128, "BK");
+  static_assert(!S2D || BK == 64, "the s2d stem uses 64-B K steps");
   constexpr int NW = WAVES_C * WAVES_P;
   constexpr int BC = 16 * WC * WAVES_C;  // channels per block tile
   constexpr int BP = 16 * WP * WAVES_P;  // pixels per block tile
   constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
   constexpr int NACC = L + LW - 1 - SMIN;
-  constexpr int WPIECES = LW * (BC / 16);
-  constexpr int APIECES = L * (BP / 16);
+  constexpr int KH = BK / 64;      // MFMA K steps per stage
+  constexpr int RPP = 1024 / BK;   // rows per 1-KiB DMA piece
+  constexpr int CPR = BK / 16;     // 16-B chunks per row
+  constexpr int WPIECES = LW * (BC / RPP);
+  constexpr int APIECES = L * (BP / RPP);
   constexpr int NPIECE = WPIECES + APIECES;
   constexpr int STAGE = NPIECE * 1024;
   constexpr int WSLOTS = (WPIECES + NW - 1) / NW;
@@ -157,25 +171,28 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
   const v4i xrs = make_rsrc(a.xq, (long long)L * a.plane);
 
   // ---- per-lane source offsets of this wave's DMA pieces -------------------------------------
-  // piece row = lane >> 2, physical chunk = lane & 3 -> logical K chunk (lane & 3) ^ swz(row)
-  const int prow = lane >> 2;
-  const int pchunk = (lane & 3) ^ swz(prow);
+  // piece row = lane / CPR, physical chunk = lane % CPR -> logical K chunk (lane % CPR) ^ swz(row),
+  // row = the row inside its 16-row MFMA block (the fragment reads' index; with BK = 128 a piece
+  // is half a block, so odd pieces start at row 8)
+  const int prow = lane / CPR;
+  auto pchunk_of = [&](int q) { return (lane % CPR) ^ swz<BK>((RPP * q + prow) & 15); };
   unsigned wsrc[WSLOTS];
 #pragma unroll
   for (int s = 0; s < WSLOTS; ++s) {
-    const int p = wave + NW * s;  // weight piece: limb p / (BC/16), block p % (BC/16)
-    const int lw = p / (BC / 16), bi = p % (BC / 16);
-    const int row = n0 + 16 * bi + prow;
+    const int p = wave + NW * s;  // weight piece: limb p / (BC/RPP), rows RPP * (p % (BC/RPP)) + ...
+    const int lw = p / (BC / RPP), bi = p % (BC / RPP);
+    const int row = n0 + RPP * bi + prow;
     wsrc[s] = (p < WPIECES && row < a.cout)
-                  ? (unsigned)((long long)lw * a.wplane + (long long)row * a.K + 16 * pchunk)
+                  ? (unsigned)((long long)lw * a.wplane + (long long)row * a.K + 16 * pchunk_of(bi))
                   : kOOB;
   }
   int apix[ASLOTS], aih[ASLOTS], aiw[ASLOTS];
 #pragma unroll
   for (int s = 0; s < ASLOTS; ++s) {
-    const int p = wave + NW * s;  // activation piece: limb p / (BP/16), block p % (BP/16)
-    const int bj = p % (BP / 16);
-    const int m = m0 + 16 * bj + prow;
+    const int p = wave + NW * s;  // activation piece: limb p / (BP/RPP), rows RPP * (p % (BP/RPP)) + ...
+    const int bj = p % (BP / RPP);
+    const int m = m0 + RPP * bj + prow;
+    const int pchunk = pchunk_of(bj);
     if (p < APIECES && m < a.M) {
       const int img = m / hw_out;
       const int rem = m - img * hw_out;
@@ -204,14 +221,14 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 #pragma unroll
     for (int s = 0; s < WSLOTS; ++s) {
       const int p = wave + NW * s;
-      if (p < WPIECES && !(kAblate & 4)) dma16(sb + p * 1024, wrs, wsrc[s], __builtin_amdgcn_readfirstlane(ks * kKStep));
+      if (p < WPIECES && !(kAblate & 4)) dma16(sb + p * 1024, wrs, wsrc[s], __builtin_amdgcn_readfirstlane(ks * BK));
     }
     const int tapoff = (kr * a.w + kc) * a.cin + c0;
 #pragma unroll
     for (int s = 0; s < ASLOTS; ++s) {
       const int p = wave + NW * s;
       if (p < APIECES && !(kAblate & 4)) {
-        const int l = p / (BP / 16);
+        const int l = p / (BP / RPP);
         unsigned voff;
         if constexpr (S2D) {
           const bool ok = (unsigned)(aih[s] + ks) < (unsigned)a.h;
@@ -240,9 +257,12 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 #pragma unroll
     for (int j = 0; j < WP; ++j) rs[l][j] = 0;
 
-  // fragment read offset inside a piece (same for every piece)
+  // fragment read offset inside a 16-row block of a [rows][BK] region, per MFMA K step h
   const int frow = lane & 15;
-  const int rd = frow * 64 + 16 * ((lane >> 4) ^ swz(frow));
+  int rd[KH];
+#pragma unroll
+  for (int h = 0; h < KH; ++h) rd[h] = frow * BK + 16 * ((4 * h + (lane >> 4)) ^ swz<BK>(frow));
+  const int nsteps = a.ksteps / KH;  // a.ksteps counts 64-wide K steps
 
   // Output coordinates of this lane: channels chan[i] + 0..3 of pixel mrow[j]; ooff = element
   // offset in an NHWC plane, or kOOB (then buffer loads read 0 and buffer stores are dropped).
@@ -320,7 +340,7 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 
   int kr = 0, kc = 0, c0 = 0;  // K position of the next step to issue
   auto advance = [&]() {
-    c0 += kKStep;
+    c0 += BK;
     if (c0 == a.cin) {
       c0 = 0;
       if (++kc == a.kw) {
@@ -332,14 +352,14 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
   int nissued = 0, wbuf = 0, rbuf = 0;
 #pragma unroll
   for (int st = 0; st < NST - 1; ++st) {
-    if (st < a.ksteps) {
+    if (st < nsteps) {
       issue(wbuf, kr, kc, c0, st);
       advance();
       ++nissued;
       wbuf = wbuf + 1 == NST ? 0 : wbuf + 1;
     }
   }
-  for (int ks = 0; ks < a.ksteps; ++ks) {
+  for (int ks = 0; ks < nsteps; ++ks) {
     // this wave's DMA of step ks has landed (the younger steps' may still fly) and its reads of
     // step ks-1 are done; after the barrier every wave's are, so stage ks is readable and the
     // stage of step ks-1 may be refilled
@@ -353,49 +373,62 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
     asm volatile("" ::: "memory");
     const int8_t* sb = lds + rbuf * STAGE;
     rbuf = rbuf + 1 == NST ? 0 : rbuf + 1;
+    // fragments of MFMA K step h of this stage (the DMA below writes the other stage, so the second
+    // half may be read after the first half's MFMAs: half the fragment registers live at a time)
     v4i wf[LW][WC], af[L][WP];
+    auto read_frags = [&](int h) {
 #pragma unroll
-    for (int lw = 0; lw < LW; ++lw)
+      for (int lw = 0; lw < LW; ++lw)
 #pragma unroll
-      for (int i = 0; i < WC; ++i)
-        wf[lw][i] = *reinterpret_cast<const v4i*>(sb + (lw * (BC / 16) + wc * WC + i) * 1024 + rd);
+        for (int i = 0; i < WC; ++i)
+          wf[lw][i] = *reinterpret_cast<const v4i*>(sb + (lw * BC + (wc * WC + i) * 16) * BK + rd[h]);
 #pragma unroll
-    for (int l = 0; l < L; ++l)
+      for (int l = 0; l < L; ++l)
 #pragma unroll
-      for (int j = 0; j < WP; ++j)
-        af[l][j] = *reinterpret_cast<const v4i*>(sb + (WPIECES + l * (BP / 16) + wp * WP + j) * 1024 + rd);
+        for (int j = 0; j < WP; ++j)
+          af[l][j] = *reinterpret_cast<const v4i*>(sb + WPIECES * 1024 + (l * BP + (wp * WP + j) * 16) * BK + rd[h]);
+    };
+    auto mma = [&]() {
+      if (do_off) {
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+#pragma unroll
+          for (int j = 0; j < WP; ++j) {
+            int s = rs[l][j];
+            s = __builtin_amdgcn_sdot4(af[l][j].x, 0x01010101, s, false);
+            s = __builtin_amdgcn_sdot4(af[l][j].y, 0x01010101, s, false);
+            s = __builtin_amdgcn_sdot4(af[l][j].z, 0x01010101, s, false);
+            s = __builtin_amdgcn_sdot4(af[l][j].w, 0x01010101, s, false);
+            rs[l][j] = s;
+          }
+      }
+#pragma unroll
+      for (int l = 0; l < L; ++l)
+#pragma unroll
+        for (int lw = 0; lw < LW; ++lw) {
+          if (l + lw < SMIN || (kAblate & 8)) continue;  // compile-time: skipped low-digit product
+#pragma unroll
+          for (int i = 0; i < WC; ++i)
+#pragma unroll
+            for (int j = 0; j < WP; ++j)
+              acc[l + lw - SMIN][i][j] =
+                  __builtin_amdgcn_mfma_i32_16x16x64_i8(wf[lw][i], af[l][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
+        }
+    };
+    read_frags(0);
     // start the DMA of step ks + NST - 1 into the stage step ks - 1 used
-    if (nissued < a.ksteps) {
+    if (nissued < nsteps) {
       issue(wbuf, kr, kc, c0, nissued);
       advance();
       ++nissued;
       wbuf = wbuf + 1 == NST ? 0 : wbuf + 1;
     }
-    if (do_off) {
+    mma();
 #pragma unroll
-      for (int l = 0; l < L; ++l)
-#pragma unroll
-        for (int j = 0; j < WP; ++j) {
-          int s = rs[l][j];
-          s = __builtin_amdgcn_sdot4(af[l][j].x, 0x01010101, s, false);
-          s = __builtin_amdgcn_sdot4(af[l][j].y, 0x01010101, s, false);
-          s = __builtin_amdgcn_sdot4(af[l][j].z, 0x01010101, s, false);
-          s = __builtin_amdgcn_sdot4(af[l][j].w, 0x01010101, s, false);
-          rs[l][j] = s;
-        }
+    for (int h = 1; h < KH; ++h) {
+      read_frags(h);
+      mma();
     }
-#pragma unroll
-    for (int l = 0; l < L; ++l)
-#pragma unroll
-      for (int lw = 0; lw < LW; ++lw) {
-        if (l + lw < SMIN || (kAblate & 8)) continue;  // compile-time: skipped low-digit product
-#pragma unroll
-        for (int i = 0; i < WC; ++i)
-#pragma unroll
-          for (int j = 0; j < WP; ++j)
-            acc[l + lw - SMIN][i][j] =
-                __builtin_amdgcn_mfma_i32_16x16x64_i8(wf[lw][i], af[l][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
-      }
   }
 
   // ---- epilogue: straight from the accumulators, in phases (uniform branches per phase) -----
@@ -591,32 +624,54 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 
 // ------------------------------------------------------------------------------------------
 struct GldsCfg {
-  int wavesc, wavesp, wc, wp, stages;
+  int wavesc, wavesp, wc, wp, stages, bk;
 };
 constexpr GldsCfg kGlds[] = {
-    {2, 2, 2, 2, 2},  // 0:  64 ch x  64 px, 256 threads
-    {2, 2, 2, 4, 2},  // 1:  64 ch x 128 px
-    {2, 2, 4, 2, 2},  // 2: 128 ch x  64 px
-    {1, 4, 4, 1, 2},  // 3:  64 ch x  64 px (each wave all 64 channels of 16 px)
-    {1, 4, 4, 2, 2},  // 4:  64 ch x 128 px
-    {4, 1, 2, 4, 2},  // 5: 128 ch x  64 px (each wave 32 ch x all 64 px)
-    {2, 2, 4, 4, 2},  // 6: 128 ch x 128 px (<= 2 accumulator sets)
-    {4, 1, 4, 2, 2},  // 7: 256 ch x  32 px (whole 256-B output rows per block: wide 1x1 expansions)
-    {4, 1, 4, 1, 2},  // 8: 256 ch x  16 px
-    {2, 2, 4, 1, 2},  // 9: 128 ch x  32 px
-    {2, 2, 2, 2, 3},  // 10: as 0, 3 LDS stages (DMA two K steps ahead; long-K 3x3 convs)
-    {1, 4, 4, 1, 3},  // 11: as 3, 3 stages
-    {2, 2, 4, 2, 3},  // 12: as 2, 3 stages
+    {2, 2, 2, 2, 2, 64},  // 0:  64 ch x  64 px, 256 threads
+    {2, 2, 2, 4, 2, 64},  // 1:  64 ch x 128 px
+    {2, 2, 4, 2, 2, 64},  // 2: 128 ch x  64 px
+    {1, 4, 4, 1, 2, 64},  // 3:  64 ch x  64 px (each wave all 64 channels of 16 px)
+    {1, 4, 4, 2, 2, 64},  // 4:  64 ch x 128 px
+    {4, 1, 2, 4, 2, 64},  // 5: 128 ch x  64 px (each wave 32 ch x all 64 px)
+    {2, 2, 4, 4, 2, 64},  // 6: 128 ch x 128 px (<= 2 accumulator sets)
+    {4, 1, 4, 2, 2, 64},  // 7: 256 ch x  32 px (whole 256-B output rows per block: wide 1x1 expansions)
+    {4, 1, 4, 1, 2, 64},  // 8: 256 ch x  16 px
+    {2, 2, 4, 1, 2, 64},  // 9: 128 ch x  32 px
+    {2, 2, 2, 2, 3, 64},  // 10: as 0, 3 LDS stages (DMA two K steps ahead; long-K 3x3 convs)
+    {1, 4, 4, 1, 3, 64},  // 11: as 3, 3 stages
+    {2, 2, 4, 2, 3, 64},  // 12: as 2, 3 stages
     // 8 waves: twice the MFMA work per loaded byte (the 3x3 convs stream ~100 ops/B from L2 at 64 x 64)
-    {2, 4, 4, 2, 2},  // 13: 128 ch x 128 px (waves 64 ch x 32 px)
-    {4, 2, 2, 4, 2},  // 14: 128 ch x 128 px (waves 32 ch x 64 px)
-    {1, 8, 4, 2, 2},  // 15:  64 ch x 256 px
-    {2, 4, 2, 4, 2},  // 16:  64 ch x 256 px (waves 32 ch x 64 px)
-    {4, 2, 4, 2, 2},  // 17: 256 ch x  64 px
+    {2, 4, 4, 2, 2, 64},  // 13: 128 ch x 128 px (waves 64 ch x 32 px)
+    {4, 2, 2, 4, 2, 64},  // 14: 128 ch x 128 px (waves 32 ch x 64 px)
+    {1, 8, 4, 2, 2, 64},  // 15:  64 ch x 256 px
+    {2, 4, 2, 4, 2, 64},  // 16:  64 ch x 256 px (waves 32 ch x 64 px)
+    {4, 2, 4, 2, 2, 64},  // 17: 256 ch x  64 px
+    // 128-B K steps (cin % 128 == 0): DMA pieces of whole cache lines
+    {2, 2, 2, 2, 2, 128},  // 18: as 0
+    {1, 4, 4, 1, 2, 128},  // 19: as 3
+    {2, 2, 4, 2, 2, 128},  // 20: as 2
+    {2, 2, 4, 1, 2, 128},  // 21: as 9
+    {1, 4, 4, 2, 2, 128},  // 22: as 4
+    {2, 4, 4, 2, 2, 128},  // 23: as 13
 };
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
 int glds_num_cfgs() { return kNumGlds; }
+
+int glds_cfg_bk(int cfg) { return kGlds[cfg].bk; }
+
+// Same rules as launch_one / launch_glds (accumulator budget, K-step width, LDS per CU).
+bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs) {
+  const GldsCfg& c = kGlds[cfg];
+  if (cin % 64 != 0 || cout % 16 != 0 || (c.bk == 128 && cin % 128 != 0)) return false;
+  if (wlimbs == 3 && limbs != 3) return false;
+  const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
+  const int accs = (limbs + wlimbs - 1 - smin) * c.wc * c.wp * 4;
+  if (accs > 128 || (accs == 128 && limbs > 1)) return false;  // (128 at 2 activation limbs spills)
+  const int stage = (wlimbs * 16 * c.wc * c.wavesc + limbs * 16 * c.wp * c.wavesp) * c.bk;
+  const int nsteps = kh * kw * cin / c.bk;
+  return (nsteps < c.stages ? nsteps : c.stages) * stage <= 160 * 1024;
+}
 
 void glds_cfg_info(int cfg, int* bm, int* bn, int* threads) {
   const GldsCfg& c = kGlds[cfg];
@@ -625,7 +680,8 @@ void glds_cfg_info(int cfg, int* bm, int* bn, int* threads) {
   *threads = 64 * c.wavesc * c.wavesp;
 }
 
-template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, bool S2D = false, int NST = 2, int MINW = 2>
+template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, bool S2D = false, int NST = 2, int MINW = 2,
+          int BK = 64>
 static int launch_one(const ConvArgs& a, hipStream_t stream) {
   constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
   if constexpr ((L + LW - 1 - SMIN) * WC * WP * 4 > 128) {
@@ -635,13 +691,22 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
     const long mt = (a.M + BP - 1) / BP;
     const long nt = (a.cout + BC - 1) / BC;
     if (mt * nt > 0x7fffffffL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
-    constexpr int STAGE = (LW * (BC / 16) + L * (BP / 16)) * 1024;
-    auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST>;
-    static const hipError_t attr =
-        hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, NST * STAGE);
-    if (attr != hipSuccess) return check_hip(attr, "qconv_glds_kernel LDS attribute");
+    if (BK == 128 && a.cin % 128 != 0)
+      return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: 128-wide K steps need cin % 128 == 0");
+    constexpr int STAGE = (LW * BC + L * BP) * BK;
+    constexpr int kMaxLds = 160 * 1024;  // LDS per CU on gfx950
+    auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK>;
     // no more stages than K steps: a single-step conv (1x1, cin 64) needs one
-    const int lds_bytes = (a.ksteps < NST ? a.ksteps : NST) * STAGE;
+    const int nsteps = a.ksteps / (BK / 64);
+    const int lds_bytes = (nsteps < NST ? nsteps : NST) * STAGE;
+    if (lds_bytes > kMaxLds) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: tile config needs more LDS than a CU has");
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+        NST * STAGE < kMaxLds ? NST * STAGE : kMaxLds);
+    if (attr != hipSuccess) {
+      (void)hipGetLastError();  // do not leave the error for the next, unrelated launch to report
+      return check_hip(attr, "qconv_glds_kernel LDS attribute");
+    }
     hipLaunchKernelGGL(kern, dim3((unsigned)(mt * nt)), dim3(64 * WAVES_C * WAVES_P), lds_bytes, stream, a);
     return check_hip(hipGetLastError(), "qconv_glds_kernel launch");
   }
@@ -668,6 +733,12 @@ static int launch_cfg(int cfg, const ConvArgs& a, hipStream_t s) {
     case 15: return launch_one<L, LW, 1, 8, 4, 2>(a, s);
     case 16: return launch_one<L, LW, 2, 4, 2, 4>(a, s);
     case 17: return launch_one<L, LW, 4, 2, 4, 2>(a, s);
+    case 18: return launch_one<L, LW, 2, 2, 2, 2, false, 2, 2, 128>(a, s);
+    case 19: return launch_one<L, LW, 1, 4, 4, 1, false, 2, 2, 128>(a, s);
+    case 20: return launch_one<L, LW, 2, 2, 4, 2, false, 2, 2, 128>(a, s);
+    case 21: return launch_one<L, LW, 2, 2, 4, 1, false, 2, 2, 128>(a, s);
+    case 22: return launch_one<L, LW, 1, 4, 4, 2, false, 2, 2, 128>(a, s);
+    case 23: return launch_one<L, LW, 2, 4, 4, 2, false, 2, 2, 128>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   }
 }

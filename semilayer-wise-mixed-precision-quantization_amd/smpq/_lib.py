@@ -57,6 +57,7 @@ _PROTOS = {
     "smpq_conv2d_num_tile_configs": (_i, []),
     "smpq_conv2d_tile_config": (_i, [_i, _vp, _vp, _vp]),
     "smpq_conv2d_tile_kind": (_i, [_i]),
+    "smpq_conv2d_tile_supported": (_i, [_i] * 7),
     "smpq_conv2d_workspace_bytes": (ctypes.c_size_t, [_i] * 10),
     "smpq_debug_mfma_i8": (_i, [_vp, _vp, _vp, _vp]),
 }

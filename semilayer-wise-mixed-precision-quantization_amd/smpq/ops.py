@@ -199,7 +199,7 @@ def tuned_stem_conv_s2d(xq, x_absmax, codes, h, w, col_scale, col_shift, relu=Tr
     if cfg is None and AUTOTUNE[0] and not torch.cuda.is_current_stream_capturing():
         best = None
         for c in tile_configs():
-            if tile_kind(c) != TILE_LDS_DMA:
+            if tile_kind(c) != TILE_LDS_DMA:  # (the stem's 16-channel pixels use 64-wide K steps)
                 continue
             try:
                 evs = []
@@ -308,7 +308,7 @@ def tile_configs():
     return _TILES
 
 
-TILE_REGSTAGE, TILE_REGSTAGE_SMALLC, TILE_LDS_DMA = 0, 1, 2  # include/smpq.h SMPQ_TILE_*
+TILE_REGSTAGE, TILE_REGSTAGE_SMALLC, TILE_LDS_DMA, TILE_LDS_DMA_K128 = 0, 1, 2, 3  # include/smpq.h SMPQ_TILE_*
 _KINDS = {}
 
 
@@ -391,19 +391,13 @@ AUTOTUNE = [os.environ.get("SMPQ_AUTOTUNE", "1") != "0"]
 _TUNED = {}
 
 
-def _tile_fits(cfg, limbs, wlimbs=1, smallc=False, cout=None):
-    bm, bn, nt = tile_configs()[cfg]
-    kind = _KINDS[cfg]
-    if smallc and kind != TILE_REGSTAGE_SMALLC:  # the cin == 4 loader exists for these tiles only
-        return False
-    waves = nt // 64
-    smin = max(0, limbs + wlimbs - 4)  # low-digit passes skipped by the kernel (see conv.hip)
-    accs = (limbs + wlimbs - 1 - smin) * (bm // 16) * (bn // 16) // waves * 4
-    if kind == TILE_LDS_DMA:
-        if cout is not None and cout % 16:
-            return False
-        return accs < 128 or (accs == 128 and limbs == 1)  # (128 at 2 activation limbs spills)
-    return accs <= 128
+def _tile_fits(cfg, limbs, wlimbs=1, smallc=False, cout=None, cin=None, k=1):
+    """Can tile config ``cfg`` run this conv (libsmpq's own launch rules)? ``cin``/``cout`` default
+    to a shape every loader takes."""
+    cin = 4 if smallc else (cin if cin is not None else 128)
+    cout = cout if cout is not None else 64
+    return bool(_lib.load().smpq_conv2d_tile_supported(int(cfg), int(cin), int(cout), int(k), int(k),
+                                                         int(limbs), int(wlimbs)))
 
 
 def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
@@ -420,7 +414,7 @@ def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, 
     if cfg is None and AUTOTUNE[0] and not torch.cuda.is_current_stream_capturing():
         best = None
         for c in tile_configs():
-            if not _tile_fits(c, limbs, wlimbs, cin == 4, cout):
+            if not _tile_fits(c, limbs, wlimbs, cin == 4, cout, cin, kh):
                 continue
             times = []
             try:

@@ -224,7 +224,7 @@ def test_all_tile_configs_bitwise_identical(gpu, shape, limbs):
     shift = torch.linspace(-1, 1, cout, device=gpu)
     outs = []
     for c in ops.tile_configs():
-        if not ops._tile_fits(c, limbs, 1, False, cout):
+        if not ops._tile_fits(c, limbs, 1, False, cout, cin, k):
             continue
         ya = torch.zeros(3, device=gpu)
         y = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, residual=res, relu=True,
@@ -232,6 +232,7 @@ def test_all_tile_configs_bitwise_identical(gpu, shape, limbs):
         outs.append((c, y, ya))
     assert len(outs) >= 3
     assert any(ops.tile_kind(c) == ops.TILE_LDS_DMA for c, _, _ in outs)
+    assert (cin % 128 != 0) or any(ops.tile_kind(c) == ops.TILE_LDS_DMA_K128 for c, _, _ in outs)
     for c, y, ya in outs[1:]:
         assert torch.equal(y, outs[0][1]), c
         assert torch.equal(ya, outs[0][2]), c
@@ -261,7 +262,7 @@ def test_static_outputs_identical_across_tiles(gpu, shape, limbs, range_frac):
     rng = float(ref.abs().max()) * range_frac
     outs = []
     for c in ops.tile_configs():
-        if not ops._tile_fits(c, limbs, 1, False, cout):
+        if not ops._tile_fits(c, limbs, 1, False, cout, cin, k):
             continue
         ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
         y, yq = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, relu=True, tile_cfg=c,
@@ -508,10 +509,10 @@ def test_conv_weight_limbs_vs_emulation(gpu, limbs, wlimbs):
     outs = []
     kinds = set()
     for c in ops.tile_configs():
-        if ops._tile_fits(c, limbs, wlimbs, False, cout):
+        if ops._tile_fits(c, limbs, wlimbs, False, cout, cin, k):
             outs.append(ops.conv2d_q(xq, am, codes, None, k, k, s, 1, cs, sh, residual=res, relu=True, tile_cfg=c))
             kinds.add(ops.tile_kind(c))
-    assert ops.TILE_LDS_DMA in kinds
+    assert ops.TILE_LDS_DMA in kinds and ops.TILE_LDS_DMA_K128 in kinds
     assert len(outs) >= 1 and all(torch.equal(o, outs[0]) for o in outs)
     wq = codes.cpu().numpy().reshape(wlimbs, cout, k, k, cin)
     rscale = (am.cpu().numpy() * np.float32(1.0 / LIMB_QMAX[limbs])).astype(np.float64)

@@ -48,14 +48,17 @@ for name, cin, cout, k, s, h, res in SHAPES:
     byt = B * h * h * cin * L + B * ho * ho * cout * L * (2 if res else 1)
     out = []
     for c in ops.tile_configs():
-        if not ops._tile_fits(c, L, 1) or (CFGS is not None and c not in CFGS):
+        if not ops._tile_fits(c, L, 1, False, cout, cin, k) or (CFGS is not None and c not in CFGS):
             continue
         kw = dict(emit_range=8.0, overflow=ovf, want_f32=False) if static else {}
         if res:
             kw.update(residual_q=rq, residual_range=4.0) if static else kw.update(
                 residual=torch.zeros(B, ho, ho, cout, device=dev))
-        for _ in range(2):
-            ops.conv2d_q(xq, am, codes, None, k, k, s, k // 2, wscale, shift, tile_cfg=c, **kw)
+        try:
+            for _ in range(2):
+                ops.conv2d_q(xq, am, codes, None, k, k, s, k // 2, wscale, shift, tile_cfg=c, **kw)
+        except Exception:  # the tile family does not take this shape
+            continue
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
         for _ in range(10):
