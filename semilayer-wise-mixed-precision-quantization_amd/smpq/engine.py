@@ -321,14 +321,30 @@ def _forward(model, x, ctx):
     return model.fc(torch.cat(feats))
 
 
+def _sig_tensors(model):
+    """(tensors, convs) the calibrated ranges and the captured graph depend on, listed once per model:
+    every conv weight and quantization metadata buffer and every BN buffer/affine parameter (the
+    reference and its drivers change weights through .data / load_state_dict — same tensor
+    objects — and never replace submodules)."""
+    st = getattr(model, "_smpq_sig_tensors", None)
+    if st is None:
+        tensors, convs = [], []
+        for m in model.modules():
+            if isinstance(m, QConv2d):
+                tensors += [m.weight, m.qstep, m.qbits]
+                convs.append(m)
+            elif isinstance(m, torch.nn.BatchNorm2d):
+                tensors += [m.running_mean, m.running_var] + ([m.weight, m.bias] if m.affine else [])
+        st = (tensors, convs)
+        model._smpq_sig_tensors = st
+    return st
+
+
 def _signature(model):
-    sig = [ops.get_act_limbs(), HEADROOM]
-    for m in model.modules():
-        if isinstance(m, QConv2d):
-            sig.append(m._pack_key())
-        elif isinstance(m, torch.nn.BatchNorm2d):
-            sig.append(_bn_key(m))
-    return tuple(sig)
+    """Value key of everything the calibrated ranges and the captured graph depend on."""
+    tensors, convs = _sig_tensors(model)
+    return (ops.get_act_limbs(), HEADROOM, tuple((t.data_ptr(), t._version) for t in tensors),
+            tuple(m._meta_gen for m in convs))
 
 
 def calibrate(model, x):
@@ -356,10 +372,18 @@ def _static_eager(model, x, cal):
     return y, ctx.overflow
 
 
+def _graph_key(model, x, cal):
+    return (tuple(x.shape), x.dtype, x.device, cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]))
+
+
+def _graph_ready(model, x, cal):
+    entry = getattr(model, "_smpq_graph", None)
+    return entry is not None and entry[0] == _graph_key(model, x, cal)
+
+
 def _graph_forward(model, x, cal):
     """Static forward through a captured HIP graph; returns (logits, overflow flag tensor)."""
-    from . import ops
-    key = (tuple(x.shape), x.dtype, x.device, cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]))
+    key = _graph_key(model, x, cal)
     entry = getattr(model, "_smpq_graph", None)
     if entry is None or entry[0] != key:
         model._smpq_graph = None
@@ -389,12 +413,22 @@ def forward_fused(model, x):
     if _MODE[0] == "dynamic":
         return _forward(model, x, None)
     cal = getattr(model, "_smpq_ranges", None)
-    if cal is None or cal[1] != _signature(model):
+    if cal is None:
         return calibrate(model, x)
-    if USE_GRAPH[0] and not torch.cuda.is_current_stream_capturing():
+    capturing = torch.cuda.is_current_stream_capturing()
+    if USE_GRAPH[0] and not capturing and _graph_ready(model, x, cal):
+        # fast path: replay first, then validate on the host while the GPU runs; a changed weight
+        # or BN buffer discards the result (recalibrate + recapture), so nothing stale is returned
         y, ovf = _graph_forward(model, x, cal)
+        if _signature(model) != cal[1]:
+            return calibrate(model, x)
     else:
-        y, ovf = _static_eager(model, x, cal)
+        if cal[1] != _signature(model):
+            return calibrate(model, x)
+        if USE_GRAPH[0] and not capturing:
+            y, ovf = _graph_forward(model, x, cal)
+        else:
+            y, ovf = _static_eager(model, x, cal)
     if int(ovf.item()) == 0:  # one sync: results are never silently clamped
         return y
     stats["overflow_reruns"] += 1

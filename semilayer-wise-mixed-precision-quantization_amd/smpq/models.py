@@ -165,6 +165,13 @@ class ResNet(nn.Module):
             return engine.forward_fused(self, x)
         return self._forward_impl(x)
 
+    def _apply(self, fn, *args, **kwargs):
+        # .to() / .cuda() / .half() replace buffer tensors: drop the engine's cached references
+        # (signature tensor list, captured graph) so they are rebuilt from the new tensors
+        for k in ("_smpq_sig_tensors", "_smpq_graph"):
+            self.__dict__.pop(k, None)
+        return super()._apply(fn, *args, **kwargs)
+
 
 def _resnet(arch, block, layers, pretrained, progress, **kwargs):
     model = ResNet(block, layers, **kwargs)

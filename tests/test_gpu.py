@@ -692,3 +692,33 @@ def test_graph_replay_matches_eager(gpu):
         g3 = net(x)   # replay
     assert stats["graph_captures"] == c0 + 1 and stats["graph_replays"] == r0 + 2
     assert torch.equal(g1, e1) and torch.equal(g2, e2) and torch.equal(g3, e1)
+
+
+def test_graph_fast_path_never_returns_stale_weights(gpu):
+    """The replay-first fast path validates weights/BN after launching: an in-place re-quantization
+    through .data (how the reference's drivers write weights) or a BN buffer change must be
+    reflected in the very next call, identical to a forward with graphs disabled."""
+    import functions
+    from smpq import engine, stats
+    net = build_model(gpu, "resnet50", "r50_mixed")
+    x = torch.randn(4, 3, 224, 224, generator=torch.Generator().manual_seed(21)).to(gpu)
+    engine.USE_GRAPH[0] = True
+    with torch.no_grad():
+        net(x)
+        net(x)  # capture
+        y0 = net(x)  # replay
+        cal0 = stats["calibrations"]
+        conv = net.layer2[1].conv2
+        functions.channel_wise_quantizationperchan(conv.weight.data, 2, 3)  # in place, no _version bump
+        y1 = net(x)
+        assert stats["calibrations"] == cal0 + 1
+        net.layer3[0].bn1.running_mean.add_(0.25)  # in-place BN buffer change
+        y2 = net(x)  # the recalibration forward (dynamic ranges)
+        assert stats["calibrations"] == cal0 + 2
+        y3, y4 = net(x), net(x)  # recapture, replay (static ranges)
+        engine.USE_GRAPH[0] = False
+        e2 = net(x)  # static ranges, eager
+        engine.USE_GRAPH[0] = True
+    assert not torch.equal(y0, y1) and not torch.equal(y1, y2)
+    assert torch.equal(y3, e2) and torch.equal(y4, e2)
+    assert (y2 - e2).abs().max() <= 2e-4 * e2.abs().max()
