@@ -722,3 +722,36 @@ def test_graph_fast_path_never_returns_stale_weights(gpu):
     assert not torch.equal(y0, y1) and not torch.equal(y1, y2)
     assert torch.equal(y3, e2) and torch.equal(y4, e2)
     assert (y2 - e2).abs().max() <= 2e-4 * e2.abs().max()
+
+
+@pytest.mark.parametrize("shape", [(64, 256, 1, 1, 20), (128, 256, 1, 1, 20), (128, 128, 3, 1, 14)],
+                         ids=lambda s: "c%d_o%d_k%d_s%d_h%d" % s)
+def test_tile_configs_deterministic(gpu, shape):
+    """Every tile config, run repeatedly on one static-range conv with a limb-plane residual and
+    both outputs, reproduces the reference config bit for bit (an intra-kernel race shows up as
+    an intermittent mismatch)."""
+    from smpq import ops
+    cin, cout, k, s, h = shape
+    limbs = 3
+    wd, step, codes, offset = make_layer(gpu, cin, cout, k, seed=cin + 5 * cout)
+    g = torch.Generator().manual_seed(11)
+    x = torch.relu(torch.randn(3, h, h, cin, generator=g)).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, limbs)
+    ho = (h + 2 * (k // 2) - k) // s + 1
+    rq = ops.act_quantize(torch.randn(3, ho, ho, cout, generator=g).clamp(-4, 4).to(gpu),
+                          torch.full((3,), 4.0, device=gpu), limbs)
+    shift = torch.linspace(-1, 1, cout, device=gpu)
+    kw = dict(residual_q=rq, residual_range=4.0, want_f32=True, relu=True)
+    ref = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, relu=True, residual_q=rq,
+                       residual_range=4.0)
+    rng = float(ref.abs().max()) * 2.0
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+    y0, q0 = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, tile_cfg=1, emit_range=rng,
+                          overflow=ovf, **kw)
+    cfgs = [c for c in ops.tile_configs() if ops._tile_fits(c, limbs, 1, False, cout, cin, k)]
+    for c in cfgs:
+        for rep in range(8):
+            y, q = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, tile_cfg=c, emit_range=rng,
+                                overflow=ovf, **kw)
+            assert torch.equal(y, y0) and torch.equal(q, q0), (c, rep)
