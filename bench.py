@@ -66,6 +66,24 @@ class ConvTimer:
             e1.record(torch.cuda.current_stream())
             self.recs.append((self._ev, e1, work))
 
+    def print_layers(self, steps):
+        """Per-launch table of the last step: time, floor T_roof and the dominant resource."""
+        n = len(self.recs) // max(steps, 1)
+        rows = []
+        for a, b, w in self.recs[-n:]:
+            t = a.elapsed_time(b) * 1e-3
+            tm = w["ops"] / (INT8_DENSE_PEAK_TOPS * 1e12)
+            th = w["bytes"] / (HBM_PEAK_GBS * 1e9)
+            rows.append((w.get("shape", "?"), t, tm, th, w["passes"]))
+        print("%-28s %9s %9s %9s %6s %8s %8s" % ("launch", "t_us", "mfma_us", "hbm_us", "roof", "TOP/s", "GB/s"),
+              file=sys.stderr)
+        for sh, t, tm, th, p in rows:
+            print("%-28s %9.1f %9.1f %9.1f %6.3f %8.1f %8.1f" % (sh, t * 1e6, tm * 1e6, th * 1e6, max(tm, th) / t,
+                                                            tm * INT8_DENSE_PEAK_TOPS / t, th * HBM_PEAK_GBS / t),
+                  file=sys.stderr)
+        tt = sum(r[1] for r in rows)
+        print("total %.1f us, floor %.1f us" % (tt * 1e6, sum(max(r[2], r[3]) for r in rows) * 1e6), file=sys.stderr)
+
     def roofline(self, steps):
         """per launch T_roof = max(ops / P_int8, bytes / BW); the reported
         bound is the resource whose floor dominates the sum."""
@@ -146,6 +164,7 @@ def main():
                     help="activation int8 limbs: 3 = int24 codes (parity mode, default), 2 = int16 (fast mode)")
     ap.add_argument("--roofline-steps", type=int, default=3, help="eager steps timed per launch for the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layers", action="store_true", help="print a per-launch roofline table (stderr)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--chunk", type=int, default=None, help="images per pass (Infinity-Cache blocking)")
     args = ap.parse_args()
@@ -222,6 +241,8 @@ def main():
     ops.set_conv_hook(None)
     engine.USE_GRAPH[0] = use_graph
     roof = timer.roofline(args.roofline_steps)
+    if args.layers and rank == 0:
+        timer.print_layers(args.roofline_steps)
 
     images = args.batch * world * args.steps
     value = images / elapsed

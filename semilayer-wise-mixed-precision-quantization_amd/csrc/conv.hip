@@ -406,7 +406,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
 #pragma unroll
         for (int s = 0; s < NACC; ++s) {
           int t = acc[s][i][j][r];
-          if (SMIN == 0 && s < L) t += coloff[j] * rsum[s];  // offsets only exist for LW == 1
+          if (SMIN == 0 && s < L) t += __mul24(coloff[j], rsum[s]);  // offsets only for LW == 1 (24-bit exact)
           v = __fmaf_rn((float)t, limbw, v);
           limbw *= 256.f;
         }

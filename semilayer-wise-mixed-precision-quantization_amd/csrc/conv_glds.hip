@@ -31,7 +31,7 @@ namespace {
 
 // Diagnostic builds only (tools/ablate_glds.sh compiles separate libraries with -DSMPQ_DIAG_ABLATE=N;
 // results are wrong with any bit set): 1 no residual loads, 2 no limb-plane stores, 4 no operand
-// DMA, 8 no MFMA.
+// DMA, 8 no MFMA, 16 no epilogue.
 #ifndef SMPQ_DIAG_ABLATE
 #define SMPQ_DIAG_ABLATE 0
 #endif
@@ -124,6 +124,59 @@ __device__ __forceinline__ unsigned pack_bytes(int b0, int b1, int b2, int b3, i
   return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// The 4 codes (channels 0..3) held by one dword per limb plane, w[l] = the 4 balanced digits of
+// limb l: q = sum_l d_l 256^l. With u_l = d_l + 128 (byte ^ 0x80) for the low limbs,
+// q = sext24(u0 | u1 << 8 | d2 << 16) - 0x8080 (L = 3), sext16(u0 | d1 << 8) - 0x80 (L = 2).
+template <int L>
+__device__ __forceinline__ void decode4(const unsigned* w, int* q) {
+  if constexpr (L == 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) q[r] = __builtin_amdgcn_sbfe((int)w[0], 8 * r, 8);
+  } else if constexpr (L == 2) {
+    const unsigned x0 = w[0] ^ 0x80808080u;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const unsigned b = __builtin_amdgcn_perm(w[1], x0, (unsigned)r | ((unsigned)(r + 4) << 8) | 0x0c0c0000u);
+      q[r] = __builtin_amdgcn_sbfe((int)b, 0, 16) - 0x80;
+    }
+  } else {
+    const unsigned x0 = w[0] ^ 0x80808080u, x1 = w[1] ^ 0x80808080u;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // [u0(2h), u1(2h), u0(2h+1), u1(2h+1)]
+      const unsigned a = __builtin_amdgcn_perm(x1, x0, h == 0 ? 0x05010400u : 0x07030602u);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int r = 2 * h + e;
+        const unsigned sel = (e == 0 ? 0x0100u : 0x0302u) | ((unsigned)(4 + r) << 16) | 0x0c000000u;
+        const unsigned b = __builtin_amdgcn_perm(w[2], a, sel);
+        q[r] = __mul24((int)b, 1) - 0x8080;  // 24-bit operand: sign from bit 23 (v_mad_i32_i24)
+      }
+    }
+  }
+}
+
+// The digit dwords of 4 clamped codes (inverse of decode4): with Q = q + 0x8080 (L = 3) / q + 0x80
+// (L = 2), digit l of q is byte l of Q, xor 0x80 for every limb below the top one.
+template <int L>
+__device__ __forceinline__ void encode4(const int* q, unsigned* w) {
+  constexpr int bias = L == 3 ? 0x8080 : (L == 2 ? 0x80 : 0);
+  const unsigned Q0 = (unsigned)(q[0] + bias), Q1 = (unsigned)(q[1] + bias), Q2 = (unsigned)(q[2] + bias),
+                 Q3 = (unsigned)(q[3] + bias);
+  const unsigned a = __builtin_amdgcn_perm(Q1, Q0, 0x05010400u);  // [Q0.b0, Q1.b0, Q0.b1, Q1.b1]
+  const unsigned b = __builtin_amdgcn_perm(Q3, Q2, 0x05010400u);
+  constexpr unsigned flip = 0x80808080u;
+  w[0] = __builtin_amdgcn_perm(b, a, 0x05040100u) ^ (L > 1 ? flip : 0u);
+  if constexpr (L >= 2) w[1] = __builtin_amdgcn_perm(b, a, 0x07060302u) ^ (L > 2 ? flip : 0u);
+  if constexpr (L >= 3) {
+    const unsigned c = __builtin_amdgcn_perm(Q1, Q0, 0x07030602u);  // [Q0.b2, Q1.b2, Q0.b3, Q1.b3]
+    const unsigned d = __builtin_amdgcn_perm(Q3, Q2, 0x07030602u);
+    w[2] = __builtin_amdgcn_perm(d, c, 0x05040100u);
+  }
+}
+
 }  // namespace
 
 // S2D: the space-to-depth stem. The image is stored as 16-channel pixels ([2x2 block][4 ch]) and
@@ -168,6 +221,11 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
   constexpr bool TRT = (WC % 4) == 0;
   constexpr int TILEB = L * BP * BC;
   extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // min(NST, ksteps) stages
+  if constexpr ((kAblate & 32) != 0) {  // diagnostic: static-range epilogue only
+    a.y = nullptr;
+    a.residual = nullptr;
+    a.y_absmax = nullptr;
+  }
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -307,7 +365,7 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
   // wave-instruction moves 64 contiguous bytes of 16 pixel rows straight from registers.
   constexpr bool TR = TRT;
   constexpr int NQ = TR ? WC / 4 : 1;
-  const bool lines = BC >= 128 || BC == a.cout;
+  const bool lines = (kAblate & 32) ? BC >= 128 : (BC >= 128 || BC == a.cout);
   const bool stage_res = TR && a.res_q && lines, stage_out = TR && a.yq && lines;
   unsigned qoff[NQ][WP];
 #pragma unroll
@@ -470,26 +528,34 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
     }
   }
 
+  if constexpr ((kAblate & 16) != 0) {  // diagnostic: no epilogue at all (keep the MFMAs live)
+    int keep = 0;
+#pragma unroll
+    for (int q = 0; q < NACC; ++q)
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) keep ^= acc[q][i][j].x ^ acc[q][i][j].w;
+    if (keep == 0x7654321) a.overflow[0] = keep;
+    return;
+  }
   // ---- epilogue: straight from the accumulators, in phases (uniform branches per phase) -----
+  // accumulator-layout dword (channels 4g..4g+3 of block wc * WC + i, pixel row of block j) of a
+  // [L][BP][BC] limb-plane tile in LDS: conflict-free for ds_read_b32 / ds_write_b32 (64 banks)
+  auto tile_word = [&](int base, int i, int j, int l) {
+    const int rt = (wp * WP + j) * 16 + frow, cc = wc * WC + i;
+    return base + l * BP * BC + rt * BC + 16 * (cc ^ swze<BC>(frow)) + 4 * (lane >> 4);
+  };
   if constexpr (TR) {
-    if (a.res_q) {
-      // the residual tile landed with the first K step (its DMA is older than every operand DMA,
-      // and the K loop's barrier made it visible): lane (g, p) reads 16 channels of block 4q + g
+    if (a.res_q && !stage_res) {
+      // lane (g, p) loaded 16 channels of block 4q + g: transpose to the accumulator layout
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
 #pragma unroll
         for (int j = 0; j < WP; ++j)
 #pragma unroll
           for (int l = 0; l < L; ++l) {
-            unsigned w0, w1, w2, w3;
-            if (stage_res) {
-              const int rt = (wp * WP + j) * 16 + frow, cc = wc * WC + 4 * q + (lane >> 4);
-              const v4i v = *reinterpret_cast<const v4i*>(lds + resoff + l * BP * BC + rt * BC +
-                                                          16 * (cc ^ swze<BC>(frow)));
-              w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-            } else {
-              w0 = rq[4 * q][j][l], w1 = rq[4 * q + 1][j][l], w2 = rq[4 * q + 2][j][l], w3 = rq[4 * q + 3][j][l];
-            }
+            unsigned w0 = rq[4 * q][j][l], w1 = rq[4 * q + 1][j][l], w2 = rq[4 * q + 2][j][l], w3 = rq[4 * q + 3][j][l];
             transpose4(w0, w1, w2, w3);
             rq[4 * q][j][l] = (int)w0;
             rq[4 * q + 1][j][l] = (int)w1;
@@ -513,6 +579,8 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 #pragma unroll
   for (int j = 0; j < WP; ++j) rscale[j] = mok[j] ? a.x_absmax[mrow[j] / hw_out] * a.inv_qmax : 0.f;
 
+  // limb recombination + affine + residual, two channels at a time (v_pk_* fp32 ops round like
+  // their scalar forms: the same bits as conv.hip's epilogue)
   float o[WC][WP][4];
 #pragma unroll
   for (int i = 0; i < WC; ++i) {
@@ -520,38 +588,47 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
     const float4 cs = *reinterpret_cast<const float4*>(a.col_scale + c);
     const float4 csh = *reinterpret_cast<const float4*>(a.col_shift + c);
     const int4 coff = do_off ? *reinterpret_cast<const int4*>(a.w_off + c) : int4{0, 0, 0, 0};
-    const float csr[4] = {cs.x, cs.y, cs.z, cs.w};
-    const float shr[4] = {csh.x, csh.y, csh.z, csh.w};
+    const f2 csr[2] = {f2{cs.x, cs.y}, f2{cs.z, cs.w}};
+    const f2 shr[2] = {f2{csh.x, csh.y}, f2{csh.z, csh.w}};
     const int cor[4] = {coff.x, coff.y, coff.z, coff.w};
 #pragma unroll
-    for (int j = 0; j < WP; ++j)
+    for (int j = 0; j < WP; ++j) {
+      int rqv[4] = {0, 0, 0, 0};
+      if (a.res_q) {
+        unsigned w[L];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = 0.f;
-        float limbw = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
+        for (int l = 0; l < L; ++l)
+          w[l] = (TR && stage_res) ? *reinterpret_cast<const unsigned*>(lds + tile_word(resoff, i, j, l))
+                                   : (unsigned)rq[i][j][l];
+        decode4<L>(w, rqv);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f2 v;
 #pragma unroll
         for (int s = 0; s < NACC; ++s) {
-          int tq = acc[s][i][j][r];
-          if (SMIN == 0 && s < L && do_off) tq += cor[r] * rs[s][j];
-          v = __fmaf_rn((float)tq, limbw, v);
-          limbw *= 256.f;
+          int t0 = acc[s][i][j][2 * h], t1 = acc[s][i][j][2 * h + 1];
+          // |offset| < 2^15 (pack_weights: |m| <= 32512), |pixel sum| < 2^22: the full-rate
+          // 24-bit multiply gives the low 32 bits of the 32-bit product
+          if (SMIN == 0 && s < L) {  // cor = 0 without offsets: no branch per element
+            t0 += __mul24(cor[2 * h], rs[s][j]);
+            t1 += __mul24(cor[2 * h + 1], rs[s][j]);
+          }
+          const f2 tf = f2{(float)t0, (float)t1};
+          constexpr float w0 = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
+          const float lw = w0 * (float)(1 << (8 * s));
+          // fma(x, 1, 0) == x for x = (float)int (never -0): the first limb is a plain convert
+          v = s == 0 ? (SMIN == 0 ? tf : tf * f2{lw, lw}) : __builtin_elementwise_fma(tf, f2{lw, lw}, v);
         }
-        o[i][j][r] = affine(v, rscale[j], csr[r], shr[r]);
+        const f2 sc = f2{rscale[j], rscale[j]} * csr[h];
+        f2 out = __builtin_elementwise_fma(v, sc, shr[h]);
+        if (a.res_q) out = out + f2{a.res_scale, a.res_scale} * f2{(float)rqv[2 * h], (float)rqv[2 * h + 1]};
+        o[i][j][2 * h] = out.x;
+        o[i][j][2 * h + 1] = out.y;
       }
+    }
   }
-  if (a.res_q) {
-#pragma unroll
-    for (int i = 0; i < WC; ++i)
-#pragma unroll
-      for (int j = 0; j < WP; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int q = 0;
-#pragma unroll
-          for (int l = L - 1; l >= 0; --l) q = q * 256 + __builtin_amdgcn_sbfe(rq[i][j][l], 8 * r, 8);
-          o[i][j][r] = __fadd_rn(o[i][j][r], __fmul_rn(a.res_scale, (float)q));
-        }
-  } else if (a.residual) {
+  if (a.residual && !a.res_q) {
     const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.residual), 0, (int)(4 * oplane),
                                                        0x00020000);
     v4u rv[WC][WP];
@@ -598,19 +675,15 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
         int q[4];
         float am = 0.f;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          q[r] = (int)fminf(fmaxf(rintf(__fmul_rn(o[i][j][r], a.yq_inv)), -qmax), qmax);
-          am = fmaxf(am, fabsf(o[i][j][r]));
+        for (int h = 0; h < 2; ++h) {
+          const f2 z = f2{o[i][j][2 * h], o[i][j][2 * h + 1]} * f2{a.yq_inv, a.yq_inv};
+          q[2 * h] = (int)fminf(fmaxf(rintf(z.x), -qmax), qmax);
+          q[2 * h + 1] = (int)fminf(fmaxf(rintf(z.y), -qmax), qmax);
         }
-        vmax = ooff[i][j] != kOOB ? fmaxf(vmax, am) : vmax;
-        unsigned wd[L];
-        wd[0] = pack_bytes(q[0], q[1], q[2], q[3], 0);
-        if constexpr (L >= 2)
-          wd[1] = pack_bytes(digit_src<1>(q[0]), digit_src<1>(q[1]), digit_src<1>(q[2]), digit_src<1>(q[3]), 1);
-        if constexpr (L >= 3)
-          wd[2] = pack_bytes(digit_src<2>(q[0]), digit_src<2>(q[1]), digit_src<2>(q[2]), digit_src<2>(q[3]), 2);
 #pragma unroll
-        for (int l = 0; l < L; ++l) wq[i][j][l] = wd[l];
+        for (int r = 0; r < 4; ++r) am = fmaxf(am, fabsf(o[i][j][r]));
+        vmax = ooff[i][j] != kOOB ? fmaxf(vmax, am) : vmax;
+        encode4<L>(q, wq[i][j]);
       }
     if (TR && !stage_out) {
 #pragma unroll
@@ -630,17 +703,11 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
       // read after this barrier), then copy it out row-major in 16-B pieces
       __syncthreads();
 #pragma unroll
-      for (int q = 0; q < NQ; ++q)
+      for (int i = 0; i < WC; ++i)
 #pragma unroll
         for (int j = 0; j < WP; ++j)
 #pragma unroll
-          for (int l = 0; l < L; ++l) {
-            unsigned w0 = wq[4 * q][j][l], w1 = wq[4 * q + 1][j][l], w2 = wq[4 * q + 2][j][l], w3 = wq[4 * q + 3][j][l];
-            transpose4(w0, w1, w2, w3);
-            const int rt = (wp * WP + j) * 16 + frow, cc = wc * WC + 4 * q + (lane >> 4);
-            *reinterpret_cast<v4i*>(lds + l * BP * BC + rt * BC + 16 * (cc ^ swze<BC>(frow))) =
-                v4i{(int)w0, (int)w1, (int)w2, (int)w3};
-          }
+          for (int l = 0; l < L; ++l) *reinterpret_cast<unsigned*>(lds + tile_word(0, i, j, l)) = wq[i][j][l];
       __syncthreads();
       constexpr int RCPR = BC / 16, ITEMS = TILEB / 16;
 #pragma unroll
