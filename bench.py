@@ -122,6 +122,22 @@ class ConvTimer:
         }
 
 
+def attach_traffic(roof, config, limbs, batch):
+    """roofline.traffic: HBM bytes per quantized-conv launch from the committed PMC measurement of
+    this workload (tools/pmc_traffic.sh: FETCH_SIZE and WRITE_SIZE passes of rocprofv3 over this
+    bench's eager roofline region, gfx950-corrected by tools/pmc_traffic.py). PMC counters cannot
+    be read from inside a normal run, so the number comes from that profile; null if absent."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic_%s_L%d_B%d.json" % (config, limbs, batch))
+    if not os.path.exists(path):
+        return
+    m = json.load(open(path))
+    if m.get("launches") != roof["launches_per_step"] * m.get("rsteps", 3):
+        return
+    roof["traffic"] = m["traffic_bytes_per_launch"]
+    roof["traffic_over_alg_bytes"] = round(m["traffic_bytes_per_launch"] / roof["alg_bytes_per_launch"], 4)
+    roof["traffic_source"] = "profiles/" + os.path.basename(path) + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
+
+
 def cpu_baseline(arch, assign_name, budget_s=12.0):
     """The reference CPU path (fp32 torch forward on the fake-quantized weights) on host cores."""
     import numpy as np
@@ -248,6 +264,7 @@ def main():
     value = images / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     roof["kernel_share_of_step"] = round(roof["conv_ms_per_step"] / ms_per_step, 4)
+    attach_traffic(roof, args.config, args.limbs, args.batch)
     if rank == 0:
         res = {
             "metric": METRIC,

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""HBM traffic per quantized-conv launch from two rocprofv3 --pmc passes over bench.py
+(FETCH_SIZE in one pass, WRITE_SIZE in another — they do not fit one pass on gfx950).
+
+Corrections (MI355X_MICROARCH.md 'HBM [CDNA4]'): FETCH_SIZE and WRITE_SIZE are in KiB;
+FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads on gfx950 (both our
+`buffer_load_dwordx4 ... lds` operand DMA and the 16-B residual loads are of that kind), so it is
+doubled; WRITE_SIZE is exact for 16-B/lane stores (the limb-plane copy-out is).
+
+The launches compared are the last `rsteps x launches` quantized-conv dispatches — bench.py's
+event-timed eager roofline region — so the traffic and `roofline.achieved` cover the same
+kernels. Writes profiles/<out>.json, which bench.py copies into roofline.traffic.
+
+usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [launches_per_step] [rsteps]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_dispatch(d, counter):
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    assert f, "no counter_collection.csv under " + d
+    rows = {}
+    for r in csv.DictReader(open(f[0])):
+        if "qconv" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            rows[int(r["Dispatch_Id"])] = (float(r["Counter_Value"]), r["Kernel_Name"])
+    return [rows[k] for k in sorted(rows)]
+
+
+def main():
+    fetch_dir, write_dir, out = sys.argv[1:4]
+    per_step = int(sys.argv[4]) if len(sys.argv) > 4 else 53
+    rsteps = int(sys.argv[5]) if len(sys.argv) > 5 else 3
+    n = per_step * rsteps
+    fe = per_dispatch(fetch_dir, "FETCH_SIZE")[-n:]
+    wr = per_dispatch(write_dir, "WRITE_SIZE")[-n:]
+    assert len(fe) == n and len(wr) == n, (len(fe), len(wr), n)
+    fetch = [2 * 1024 * v for v, _ in fe]
+    write = [1024 * v for v, _ in wr]
+    res = {
+        "launches": n,
+        "rsteps": rsteps,
+        "fetch_bytes_per_launch": round(sum(fetch) / n),
+        "write_bytes_per_launch": round(sum(write) / n),
+        "traffic_bytes_per_launch": round((sum(fetch) + sum(write)) / n),
+        "per_step_launch_bytes": [round(f + w) for f, w in zip(fetch[-per_step:], write[-per_step:])],
+        "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read half count), WRITE_SIZE KiB x 1024",
+    }
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "per_step_launch_bytes"}))
+
+
+if __name__ == "__main__":
+    main()
