@@ -24,6 +24,9 @@
  *   smpq_act_absmax                (new) per-image activation range for the activation quantizer
  *   smpq_act_quantize              (new) activation quantizer (the reference keeps fp32 activations;
  *                                  int16/int24 codes reproduce them within the stated tolerance)
+ *   smpq_softmax_xent              per-batch body of functions.py:84-129 evaluate_acc_loss_softmax
+ *                                  (output.max(1), CrossEntropyLoss, Softmax(dim=1), :113-121)
+ *   smpq_kl_rows                   functions.py:131-149 KLdiv (per-image sum_c n*log(n/o), :140-146)
  */
 #ifndef SMPQ_H_
 #define SMPQ_H_
@@ -219,6 +222,22 @@ int smpq_conv2d_tile_supported(int cfg, int cin, int cout, int kh, int kw, int l
 /* Workspace the conv needs (none today; kept for ABI stability). */
 size_t smpq_conv2d_workspace_bytes(int n, int h, int w, int cin, int cout, int kh, int kw,
                                    int stride, int pad, int limbs);
+
+/* ---- evaluation reductions (functions.py:84-149) ---------------------------------------------
+ * smpq_softmax_xent: one batch of logits [rows][cols] fp32 with int64 labels [rows]:
+ *   probs  fp32 [rows][cols] softmax = exp(x - max) / sum (functions.py:117), or NULL
+ *   stats  double [4], ACCUMULATED (+=): [0] batch-mean cross entropy (criterion(output, y),
+ *          :116 — one term per call, as loss_sum += loss at :121), [1] rows whose first maximal
+ *          class equals the label (output.max(1), :114), [2] rows, [3] batches (+1)
+ *   row_ws fp32 workspace [2 * rows]
+ * smpq_kl_rows: stats double [2] += {sum over rows of sum_c p_ref * log(p_ref / p), rows}
+ *   (functions.py:140-146; KLdiv = stats[0] / stats[1]); row_ws fp32 [rows].
+ * Rows are reduced in a fixed order in double: results do not depend on launch timing. A label
+ * outside [0, cols) makes that row's loss NaN (the reference raises). */
+int smpq_softmax_xent(const float* logits, const int64_t* labels, int rows, int cols, float* probs,
+                      double* stats, float* row_ws, smpq_stream_t stream);
+int smpq_kl_rows(const float* p_ref, const float* p, int rows, int cols, double* stats, float* row_ws,
+                 smpq_stream_t stream);
 
 /* Diagnostics: one v_mfma_i32_16x16x64_i8 with the kernel's fragment mapping.
  *   a [16][64] int8 row-major, b [16][64] int8 (b[col][k]), c [16][16] int32 row-major */

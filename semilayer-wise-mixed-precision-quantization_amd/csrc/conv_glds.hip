@@ -428,6 +428,11 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
                                                                                   (unsigned)((long long)l * oplane), 0);
   }
 
+  // per-pixel activation scale (per-image range): loaded now, used in the epilogue
+  float rscale[WP];
+#pragma unroll
+  for (int j = 0; j < WP; ++j) rscale[j] = mok[j] ? a.x_absmax[mrow[j] / hw_out] * a.inv_qmax : 0.f;
+
   // DMA pieces this wave issues per K step (wave-uniform): the counted vmcnt below
   int ppw = 0;
 #pragma unroll
@@ -575,10 +580,40 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
         rs[l][j] = s;
       }
   }
-  float rscale[WP];
+  if constexpr (SMIN == 0) {
+    if (do_off) {  // weight offsets (8-bit channels off-centre): acc_l += offset_c * sum of pixel digits_l
 #pragma unroll
-  for (int j = 0; j < WP; ++j) rscale[j] = mok[j] ? a.x_absmax[mrow[j] / hw_out] * a.inv_qmax : 0.f;
-
+      for (int i = 0; i < WC; ++i) {
+        const int c = chan[i] < a.cout ? chan[i] : 0;
+        const int4 coff = *reinterpret_cast<const int4*>(a.w_off + c);
+        const int cor[4] = {coff.x, coff.y, coff.z, coff.w};
+#pragma unroll
+        for (int s = 0; s < L; ++s)
+#pragma unroll
+          for (int j = 0; j < WP; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)  // |offset| < 2^15, |pixel sum| < 2^22: full-rate 24-bit multiply
+              acc[s][i][j][r] += __mul24(cor[r], rs[s][j]);
+      }
+    }
+  }
+  // residual limb planes -> codes, all at once (one LDS wait instead of one per block)
+  int rqv[WC][WP][4];
+  if (a.res_q) {
+    unsigned rw[WC][WP][L];
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j)
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+          rw[i][j][l] = (TR && stage_res) ? *reinterpret_cast<const unsigned*>(lds + tile_word(resoff, i, j, l))
+                                          : (unsigned)rq[i][j][l];
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j) decode4<L>(rw[i][j], rqv[i][j]);
+  }
   // limb recombination + affine + residual, two channels at a time (v_pk_* fp32 ops round like
   // their scalar forms: the same bits as conv.hip's epilogue)
   float o[WC][WP][4];
@@ -587,33 +622,16 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
     const int c = chan[i] < a.cout ? chan[i] : 0;
     const float4 cs = *reinterpret_cast<const float4*>(a.col_scale + c);
     const float4 csh = *reinterpret_cast<const float4*>(a.col_shift + c);
-    const int4 coff = do_off ? *reinterpret_cast<const int4*>(a.w_off + c) : int4{0, 0, 0, 0};
     const f2 csr[2] = {f2{cs.x, cs.y}, f2{cs.z, cs.w}};
     const f2 shr[2] = {f2{csh.x, csh.y}, f2{csh.z, csh.w}};
-    const int cor[4] = {coff.x, coff.y, coff.z, coff.w};
 #pragma unroll
     for (int j = 0; j < WP; ++j) {
-      int rqv[4] = {0, 0, 0, 0};
-      if (a.res_q) {
-        unsigned w[L];
-#pragma unroll
-        for (int l = 0; l < L; ++l)
-          w[l] = (TR && stage_res) ? *reinterpret_cast<const unsigned*>(lds + tile_word(resoff, i, j, l))
-                                   : (unsigned)rq[i][j][l];
-        decode4<L>(w, rqv);
-      }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         f2 v;
 #pragma unroll
         for (int s = 0; s < NACC; ++s) {
-          int t0 = acc[s][i][j][2 * h], t1 = acc[s][i][j][2 * h + 1];
-          // |offset| < 2^15 (pack_weights: |m| <= 32512), |pixel sum| < 2^22: the full-rate
-          // 24-bit multiply gives the low 32 bits of the 32-bit product
-          if (SMIN == 0 && s < L) {  // cor = 0 without offsets: no branch per element
-            t0 += __mul24(cor[2 * h], rs[s][j]);
-            t1 += __mul24(cor[2 * h + 1], rs[s][j]);
-          }
+          const int t0 = acc[s][i][j][2 * h], t1 = acc[s][i][j][2 * h + 1];
           const f2 tf = f2{(float)t0, (float)t1};
           constexpr float w0 = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
           const float lw = w0 * (float)(1 << (8 * s));
@@ -622,7 +640,8 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
         }
         const f2 sc = f2{rscale[j], rscale[j]} * csr[h];
         f2 out = __builtin_elementwise_fma(v, sc, shr[h]);
-        if (a.res_q) out = out + f2{a.res_scale, a.res_scale} * f2{(float)rqv[2 * h], (float)rqv[2 * h + 1]};
+        if (a.res_q)
+          out = out + f2{a.res_scale, a.res_scale} * f2{(float)rqv[i][j][2 * h], (float)rqv[i][j][2 * h + 1]};
         o[i][j][2 * h] = out.x;
         o[i][j][2 * h + 1] = out.y;
       }

@@ -2,9 +2,10 @@
 
 Same names, signatures and return values:
   quantize_wgt, channel_wise_quantizationperchan      -> smpq.quant (libsmpq, bit-exact)
-  evaluate_loss, evaluate_acc_loss_softmax             -> GPU eval loop over net(x), one host
+  evaluate_loss, evaluate_acc_loss_softmax             -> GPU eval loop over net(x) + the fused
+                                                          softmax / CE / top-1 kernel, one host
                                                           sync per call instead of per batch
-  KLdiv                                                -> batched on device (same formula)
+  KLdiv                                                -> smpq_kl_rows on device (same formula)
   make_divide_minusplusmodels, make_quantizedlists,
   make_semilayers_resnet18/34/50                       -> the search bookkeeping, restated
 The reference's quirks that change results are kept on purpose (they are what a drop-in must
@@ -14,57 +15,62 @@ pass quantizing the caller's net for its first semilayer before switching to fre
 """
 import torch
 
+from smpq import ops
 from smpq.quant import channel_wise_quantizationperchan, quantize_wgt  # noqa: F401
 
 _SENTINEL = [0, 0, 100, 0, 0, 0, 0, 0]
 
 
-def _run_eval(net, device, data_loader):
+def _run_eval(net, device, data_loader, want_probs):
+    """Forward every batch, then the fused softmax / cross-entropy / top-1 kernel
+    (smpq_softmax_xent) accumulates [loss_sum, correct, seen, batches] on the device: one host
+    sync per evaluation. Returns (stats float64 [4] on the device, list of softmax outputs)."""
     net.to(device)
     net.eval()
-    criterion = torch.nn.CrossEntropyLoss()
-    correct = None
-    loss_sum = None
-    seen = 0
-    count = 0
+    dev = torch.device(device)
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    stats = torch.zeros(4, dtype=torch.float64, device=dev)
     outputs = []
     with torch.no_grad():
         for x, y in data_loader:
             x = x.to(device, non_blocking=True)
-            y = y.to(device, non_blocking=True)
-            out = net(x)
-            pred = out.argmax(1)
-            loss = criterion(out, y)
-            hit = (pred == y).sum()
-            correct = hit if correct is None else correct + hit
-            loss_sum = loss if loss_sum is None else loss_sum + loss
-            seen += y.numel()
-            count += 1
-            outputs.append(out)
-    return correct, loss_sum, seen, count, outputs
+            out = net(x).float().contiguous()
+            p = ops.softmax_xent(out, y, stats, want_probs=want_probs)
+            if want_probs:
+                outputs.append(p)
+    return stats, outputs
+
+
+def _finish(stats):
+    loss_sum, correct, seen, count = stats.tolist()  # the one host sync
+    return correct / seen, loss_sum / count
 
 
 def evaluate_loss(net, device, data_loader):
     """functions.py:45-82: mean over batches of the batch CE loss (the reference's second,
     redundant forward per batch at :71 only recomputed the prediction, so it is not repeated)."""
-    _, loss_sum, _, count, _ = _run_eval(net, device, data_loader)
-    return (loss_sum / count).item()
+    stats, _ = _run_eval(net, device, data_loader, want_probs=False)
+    return _finish(stats)[1]
 
 
 def evaluate_acc_loss_softmax(net, device, data_loader):
     """functions.py:84-129: (top-1 accuracy, mean batch loss, list of per-batch softmax)."""
-    correct, loss_sum, seen, count, outs = _run_eval(net, device, data_loader)
-    softmax = torch.nn.Softmax(dim=1)
-    outputs = [softmax(o) for o in outs]
-    acc = correct.float() / seen
-    loss = loss_sum / count
-    return acc.item(), loss.item(), outputs
+    stats, outs = _run_eval(net, device, data_loader, want_probs=True)
+    acc, loss = _finish(stats)
+    return acc, loss, outs
 
 
 def KLdiv(n_out, out):
-    """functions.py:131-149: mean over images of sum_c p_c * log(p_c / q_c)."""
-    kls = [(p * (p / q).log()).sum(dim=1) for p, q in zip(n_out, out)]
-    return torch.cat(kls).mean().item()
+    """functions.py:131-149: mean over images of sum_c p_c * log(p_c / q_c) (smpq_kl_rows per
+    batch pair, accumulated on the device, one host sync)."""
+    stats = None
+    for p, q in zip(n_out, out):
+        if stats is None:
+            stats = torch.zeros(2, dtype=torch.float64, device=q.device)
+        ops.kl_rows(p.to(q.device), q, stats)
+    s, n = stats.tolist()
+    return s / n
 
 
 def make_divide_minusplusmodels(paramlists, dlists, index):

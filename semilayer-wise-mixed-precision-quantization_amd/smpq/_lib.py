@@ -60,6 +60,8 @@ _PROTOS = {
     "smpq_conv2d_tile_supported": (_i, [_i] * 7),
     "smpq_conv2d_workspace_bytes": (ctypes.c_size_t, [_i] * 10),
     "smpq_debug_mfma_i8": (_i, [_vp, _vp, _vp, _vp]),
+    "smpq_softmax_xent": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp]),
+    "smpq_kl_rows": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp]),
 }
 
 EXPORTED_SYMBOLS = tuple(_PROTOS)

@@ -32,3 +32,47 @@ def sharded_forward(fn, x_global, rank, world):
     s, e = shard_range(x_global.shape[0], rank, world)
     assert (e - s) * world == x_global.shape[0], "equal shards required for all_gather_into_tensor"
     return gather_logits(fn(x_global[s:e]), world)
+
+
+def all_reduce_stats(stats, world):
+    """Sum per-rank evaluation accumulators (smpq_softmax_xent's [loss_sum, correct, seen,
+    batches] or smpq_kl_rows' [kl_sum, rows], float64) over ranks: the only collective the
+    sharded evaluation needs (SURVEY.md 8(f) rank 1 — a few scalars instead of the logits)."""
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+    return stats
+
+
+def sharded_eval(net, loader, rank, world, device=None, keep_probs=True):
+    """functions.evaluate_acc_loss_softmax (functions.py:84-129) with every global batch split
+    over the ranks (equal shards): each rank forwards its images, the fused softmax / CE / top-1
+    kernel accumulates on its device, and one all-reduce of 4 doubles combines the ranks.
+    Returns (acc, loss, this rank's softmax shards) — the shards stay where they were made and
+    feed sharded_kldiv, so no logits or probabilities cross xGMI."""
+    from smpq import ops
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    stats = torch.zeros(4, dtype=torch.float64, device=dev)
+    probs = []
+    with torch.no_grad():
+        for x, y in loader:
+            s, e = shard_range(x.shape[0], rank, world)
+            assert (e - s) * world == x.shape[0], "equal shards required (the batch mean of shard means)"
+            out = net(x[s:e].to(dev, non_blocking=True)).float().contiguous()
+            p = ops.softmax_xent(out, y[s:e], stats, want_probs=keep_probs)
+            if keep_probs:
+                probs.append(p)
+    loss_sum, correct, seen, count = all_reduce_stats(stats, world).tolist()
+    return correct / seen, loss_sum / count, probs
+
+
+def sharded_kldiv(n_out_local, out_local, world):
+    """functions.KLdiv (functions.py:131-149) over softmax shards held per rank: per-rank
+    smpq_kl_rows sums, then one all-reduce of 2 doubles."""
+    from smpq import ops
+    stats = None
+    for p, q in zip(n_out_local, out_local):
+        if stats is None:
+            stats = torch.zeros(2, dtype=torch.float64, device=q.device)
+        ops.kl_rows(p, q, stats)
+    s, n = all_reduce_stats(stats, world).tolist()
+    return s / n

@@ -486,3 +486,38 @@ def debug_mfma_i8(a, b):
         _lib.check(lib.smpq_debug_mfma_i8(_lib.ptr(a.contiguous()), _lib.ptr(b.contiguous()), _lib.ptr(c),
                                           _lib.stream_ptr()), "smpq_debug_mfma_i8")
     return c
+
+
+# ---- evaluation reductions (functions.py:84-149) on device -----------------------------------
+def softmax_xent(logits, labels, stats, want_probs=True):
+    """One batch of functions.evaluate_acc_loss_softmax (functions.py:113-121) in one kernel:
+    returns the softmax [B, C] fp32 (or None) and accumulates into ``stats`` (float64 [4], on the
+    logits' device): [0] += batch-mean cross entropy, [1] += correct top-1, [2] += rows, [3] += 1."""
+    _req(logits.is_cuda and logits.dtype == torch.float32 and logits.dim() == 2 and logits.is_contiguous(),
+         "softmax_xent: logits must be a contiguous fp32 [B, C] device tensor")
+    rows, cols = logits.shape
+    labels = labels.to(device=logits.device, dtype=torch.int64).contiguous()
+    _req(labels.numel() == rows, "softmax_xent: labels")
+    _req(stats.dtype == torch.float64 and stats.numel() >= 4 and stats.device == logits.device, "softmax_xent: stats")
+    probs = torch.empty_like(logits) if want_probs else None
+    ws = torch.empty(2 * max(rows, 1), dtype=torch.float32, device=logits.device)
+    with torch.cuda.device(logits.device):
+        _lib.check(_lib.load().smpq_softmax_xent(_lib.ptr(logits), _lib.ptr(labels), rows, cols, _lib.ptr(probs),
+                                                 _lib.ptr(stats), _lib.ptr(ws), _lib.stream_ptr()),
+                   "smpq_softmax_xent")
+    return probs
+
+
+def kl_rows(p_ref, p, stats):
+    """functions.KLdiv (functions.py:131-149) for one batch pair: stats (float64 [2]) +=
+    (sum over images of sum_c p_ref * log(p_ref / p), images)."""
+    for t in (p_ref, p):
+        _req(t.is_cuda and t.dtype == torch.float32 and t.dim() == 2, "kl_rows: fp32 [B, C] device tensors")
+    _req(p_ref.shape == p.shape and p_ref.device == p.device, "kl_rows: shapes")
+    p_ref, p = p_ref.contiguous(), p.contiguous()
+    _req(stats.dtype == torch.float64 and stats.numel() >= 2 and stats.device == p.device, "kl_rows: stats")
+    rows, cols = p.shape
+    ws = torch.empty(max(rows, 1), dtype=torch.float32, device=p.device)
+    with torch.cuda.device(p.device):
+        _lib.check(_lib.load().smpq_kl_rows(_lib.ptr(p_ref), _lib.ptr(p), rows, cols, _lib.ptr(stats), _lib.ptr(ws),
+                                            _lib.stream_ptr()), "smpq_kl_rows")

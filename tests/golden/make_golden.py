@@ -6,6 +6,8 @@ Writes (all data, no reference source):
   tests/golden/quant_kat.npz          quantize_wgt known-answer vectors (functions.py:25-43)
   tests/golden/model_goldens.npz      logits of seeded reference models on seeded inputs,
                                       per-conv weight checksums, BN state of the parity models
+  tests/golden/eval_golden.npz        evaluate_acc_loss_softmax / KLdiv (functions.py:84-149) of
+                                      the reference on seeded logits (run alone: `... eval`)
   <pkg>/smpq/data/assign_*.npz        per-channel bit/chain assignments for the bench configs
                                       (R50 reconstruction: SURVEY.md Appendix B)
 
@@ -310,9 +312,36 @@ def make_model_goldens(functions, resnet, assigns):
     np.savez_compressed(os.path.join(HERE, "model_goldens.npz"), **out)
 
 
+def make_eval_golden(functions):
+    """The reference's evaluate_acc_loss_softmax + KLdiv on seeded logits: the 'net' is an
+    identity module and each loader item's x IS the logits batch (ragged last batch, a tied row)."""
+    g = torch.Generator().manual_seed(7)
+    sizes = [16, 16, 5]
+    la, lb, ys = [], [], []
+    for b in sizes:
+        a = torch.randn(b, 1000, generator=g) * 3.0
+        a[0, 10] = a[0, 500] = a[0].max() + 1.0  # tie: the first maximal class wins
+        la.append(a)
+        lb.append(a + 0.3 * torch.randn(b, 1000, generator=g))
+        ys.append(torch.randint(0, 1000, (b,), generator=g))
+    ys[0][0] = 10
+    net = torch.nn.Identity()
+    acc_a, loss_a, out_a = functions.evaluate_acc_loss_softmax(net, "cpu", list(zip(la, ys)))
+    acc_b, loss_b, out_b = functions.evaluate_acc_loss_softmax(net, "cpu", list(zip(lb, ys)))
+    kl = functions.KLdiv(out_a, out_b)
+    np.savez_compressed(os.path.join(HERE, "eval_golden.npz"), sizes=np.array(sizes),
+                        logits_a=torch.cat(la).numpy(), logits_b=torch.cat(lb).numpy(),
+                        labels=torch.cat(ys).numpy(), acc_a=acc_a, loss_a=loss_a, acc_b=acc_b, loss_b=loss_b,
+                        softmax_a=torch.cat(out_a).numpy(), softmax_b=torch.cat(out_b).numpy(), kl=kl)
+
+
 def main():
     os.makedirs(PKG_DATA, exist_ok=True)
     functions, resnet = import_reference()
+    if sys.argv[1:] == ["eval"]:
+        make_eval_golden(functions)
+        return
+    make_eval_golden(functions)
     assigns = {"r50_mixed": reconstruct_r50_mixed(), "r18_u8": r18_uniform8(),
                "r34_4bit": r34_4bit_dominant()}
     save_assignment("r50_mixed", "resnet50", *assigns["r50_mixed"])

@@ -67,3 +67,62 @@ def test_shard_range_covers_batch():
             spans = [dp.shard_range(b, r, w) for r in range(w)]
             assert spans[0][0] == 0 and spans[-1][1] == b
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+
+
+def _stats_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "semilayer-wise-mixed-precision-quantization_amd"))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import numpy as np
+        from oracle import eval_ref
+        from smpq import dp
+        # each rank holds its shard of every global batch; per-rank accumulators as the kernel
+        # (smpq_softmax_xent) forms them: [sum of shard-mean CE, correct, rows, batches]
+        g = torch.Generator().manual_seed(5)
+        st = torch.zeros(4, dtype=torch.float64)
+        for _ in range(3):
+            x = torch.randn(8, 50, generator=g).numpy()
+            y = torch.randint(0, 50, (8,), generator=g).numpy()
+            s, e = dp.shard_range(8, rank, world)
+            acc, loss, _ = eval_ref.evaluate_acc_loss_softmax([(x[s:e], y[s:e])])
+            st += torch.tensor([loss, acc * (e - s), e - s, 1.0], dtype=torch.float64)
+        q.put((rank, dp.all_reduce_stats(st, world).tolist()))
+        del np
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_eval_stats_all_reduce_equals_single_process():
+    """The sharded evaluation's only collective: 4 doubles summed over ranks reproduce the
+    single-process accuracy and mean batch loss of functions.py:84-129 (equal shards)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import eval_ref
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stats_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = torch.Generator().manual_seed(5)
+    batches = []
+    for _ in range(3):
+        x = torch.randn(8, 50, generator=g).numpy()
+        y = torch.randint(0, 50, (8,), generator=g).numpy()
+        batches.append((x, y))
+    acc, loss, _ = eval_ref.evaluate_acc_loss_softmax(batches)
+    for r in range(world):
+        loss_sum, correct, seen, count = res[r]
+        assert res[r] == res[0]
+        assert abs(correct / seen - acc) < 1e-12
+        assert abs(loss_sum / count - loss) < 1e-9

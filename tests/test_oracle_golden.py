@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from conftest import GOLDEN
-from oracle import forward_ref, quant_ref
+from oracle import eval_ref, forward_ref, quant_ref
 
 
 def _kat():
@@ -114,3 +114,24 @@ def test_torch_oracle_reproduces_reference_logits():
         out = torch_ref.resnet_forward(arch, sd, x).numpy()
         ref = g[case + "/logits"]
         assert np.abs(out - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+def _eval_golden():
+    z = np.load(os.path.join(GOLDEN, "eval_golden.npz"), allow_pickle=False)
+    cuts = np.cumsum([0] + list(z["sizes"]))
+    split = lambda a: [a[cuts[i]:cuts[i + 1]] for i in range(len(cuts) - 1)]  # noqa: E731
+    return z, split
+
+
+def test_eval_oracle_vs_reference():
+    # functions.py:84-149 run by the reference itself on seeded logits (ragged batch, tied row)
+    z, split = _eval_golden()
+    batches = list(zip(split(z["logits_a"]), split(z["labels"])))
+    acc, loss, outs = eval_ref.evaluate_acc_loss_softmax(batches)
+    assert abs(acc - float(z["acc_a"])) < 1e-7  # the reference divides in fp32 (functions.py:125)
+    assert abs(loss - float(z["loss_a"])) < 1e-5 * abs(float(z["loss_a"]))
+    np.testing.assert_allclose(np.concatenate(outs), z["softmax_a"], rtol=1e-5, atol=1e-9)
+    acc_b, loss_b, outs_b = eval_ref.evaluate_acc_loss_softmax(list(zip(split(z["logits_b"]), split(z["labels"]))))
+    assert abs(acc_b - float(z["acc_b"])) < 1e-7 and abs(loss_b - float(z["loss_b"])) < 1e-5 * abs(float(z["loss_b"]))
+    kl = eval_ref.kldiv(split(z["softmax_a"]), split(z["softmax_b"]))
+    assert abs(kl - float(z["kl"])) < 1e-5 * abs(float(z["kl"]))
