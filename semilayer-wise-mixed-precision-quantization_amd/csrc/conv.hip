@@ -437,7 +437,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
       const float4 v = *reinterpret_cast<const float4*>(&tile[r * TS + 4 * c4]);
       float* dst = a.y + (size_t)m * a.cout + col;
       if (vec_ok && col + 3 < a.cout) {
-        *reinterpret_cast<float4*>(dst) = v;
+        st16(dst, v4i{__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w)});
       } else {
         dst[0] = v.x;
         if (col + 1 < a.cout) dst[1] = v.y;
@@ -478,8 +478,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(Con
       if (col + 15 < a.cout) {
 #pragma unroll
         for (int l = 0; l < L; ++l)
-          *reinterpret_cast<v4i*>(dq + l * yplane) =
-              v4i{(int)word[l][0], (int)word[l][1], (int)word[l][2], (int)word[l][3]};
+          st16(dq + l * yplane, v4i{(int)word[l][0], (int)word[l][1], (int)word[l][2], (int)word[l][3]});
       } else {
         for (int l = 0; l < L; ++l)
           for (int k = 0; k < 16 && col + k < a.cout; ++k)
@@ -618,8 +617,7 @@ __global__ __launch_bounds__(256) void image_quantize_s2d_kernel(const float* __
     }
 #pragma unroll
     for (int l = 0; l < L; ++l)
-      *reinterpret_cast<v4i*>(out + l * plane + 16 * p) =
-          v4i{(int)word[l][0], (int)word[l][1], (int)word[l][2], (int)word[l][3]};
+      st16(out + l * plane + 16 * p, v4i{(int)word[l][0], (int)word[l][1], (int)word[l][2], (int)word[l][3]});
   }
 }
 
@@ -661,7 +659,7 @@ __global__ __launch_bounds__(256) void maxpool_quantize_kernel(const float* __re
       }
     }
     const size_t o = (((size_t)img * ho + oh) * wo + ow) * c + 4 * cq;
-    if (out_f32) *reinterpret_cast<float4*>(out_f32 + o) = m;
+    if (out_f32) st16(out_f32 + o, v4i{__float_as_int(m.x), __float_as_int(m.y), __float_as_int(m.z), __float_as_int(m.w)});
     const float am = absmax[img];
     const float inv = am > 0.f ? qmax / am : 0.f;
     const float vals[4] = {m.x, m.y, m.z, m.w};
@@ -688,51 +686,51 @@ template <int L>
 __global__ __launch_bounds__(256) void maxpool_limbs_kernel(const int8_t* __restrict__ x, int n, int h, int w, int c,
                                                             int ho, int wo, long long iplane,
                                                             int8_t* __restrict__ out, long long oplane) {
+  // one thread = 16 channels of one pooled pixel; all 9 taps x L limbs are loaded before any is
+  // used (27 independent 16-B loads in flight). A tap outside the image re-reads the window's
+  // centre (2 oh, 2 ow), which is always inside and already part of the max: no masks.
   const int c16 = c / 16;
-  const long long total = (long long)n * ho * wo * c16;
-  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (long long)gridDim.x * blockDim.x) {
-    const int cq = (int)(t % c16);
-    long long p = t / c16;
-    const int ow = (int)(p % wo);
-    p /= wo;
-    const int oh = (int)(p % ho);
-    const int img = (int)(p / ho);
-    int m[16];
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;  // total < 2^31 (checked by the launcher)
+  if (t >= n * ho * wo * c16) return;
+  const int cq = t % c16;
+  int p = t / c16;
+  const int ow = p % wo;
+  p /= wo;
+  const int oh = p % ho;
+  const int img = p / ho;
+  const long long base = (long long)img * h * w;
+  v4i d[9][L];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) m[k] = INT_MIN;
-    for (int dr = 0; dr < 3; ++dr) {
-      const int ih = 2 * oh - 1 + dr;
-      if ((unsigned)ih >= (unsigned)h) continue;
-      for (int dc = 0; dc < 3; ++dc) {
-        const int iw = 2 * ow - 1 + dc;
-        if ((unsigned)iw >= (unsigned)w) continue;
-        const size_t off = (((size_t)img * h + ih) * w + iw) * c + 16 * cq;
-        v4i d[L];
-#pragma unroll
-        for (int l = 0; l < L; ++l) d[l] = *reinterpret_cast<const v4i*>(x + l * iplane + off);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          int q = 0;
-#pragma unroll
-          for (int l = L - 1; l >= 0; --l) q = q * 256 + (int)(int8_t)((unsigned)d[l][k >> 2] >> (8 * (k & 3)));
-          m[k] = max(m[k], q);
-        }
-      }
+  for (int tap = 0; tap < 9; ++tap) {
+    int ih = 2 * oh - 1 + tap / 3, iw = 2 * ow - 1 + tap % 3;
+    if ((unsigned)ih >= (unsigned)h || (unsigned)iw >= (unsigned)w) {
+      ih = 2 * oh;
+      iw = 2 * ow;
     }
-    const size_t o = (((size_t)img * ho + oh) * wo + ow) * c + 16 * cq;
+    const long long off = ((base + (long long)ih * w + iw) * c) + 16 * cq;
 #pragma unroll
-    for (int l = 0; l < L; ++l) {
-      unsigned wd[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        int dg[L];
-        split_limbs<L>(m[k], dg);
-        wd[k >> 2] |= (unsigned)(dg[l] & 255) << (8 * (k & 3));
-      }
-      *reinterpret_cast<v4i*>(out + l * oplane + o) = v4i{(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
-    }
+    for (int l = 0; l < L; ++l) d[tap][l] = *reinterpret_cast<const v4i*>(x + l * iplane + off);
   }
+  int m[16];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      unsigned wv[L];
+#pragma unroll
+      for (int l = 0; l < L; ++l) wv[l] = (unsigned)d[tap][l][k];
+      int q[4];
+      decode4<L>(wv, q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) m[4 * k + r] = tap == 0 ? q[r] : max(m[4 * k + r], q[r]);
+    }
+  const long long o = (((long long)img * ho + oh) * wo + ow) * c + 16 * cq;
+  unsigned wd[4][L];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) encode4<L>(&m[4 * k], wd[k]);
+#pragma unroll
+  for (int l = 0; l < L; ++l)
+    st16(out + l * oplane + o, v4i{(int)wd[0][l], (int)wd[1][l], (int)wd[2][l], (int)wd[3][l]});
 }
 
 __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, int64_t per_image,
@@ -886,7 +884,7 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
   if (wlimbs < 1 || wlimbs > 3) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: wlimbs must be 1, 2 or 3");
   if (wlimbs == 3 && limbs != 3)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: 3 weight limbs are built for 3 activation limbs only");
-  ConvArgs a;
+  ConvArgs a = {};
   a.s2d = 0;
   a.xq = xq;
   a.plane = (long long)n * h * w * cin;
@@ -932,6 +930,14 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
   a.wplane = (long long)cout * a.K;
   a.relu = relu ? 1 : 0;
   a.has_offset = (offset && wlimbs == 1) ? 1 : 0;
+  {
+    // outputs larger than this stream past the 256-MB MALL anyway: store them non-temporally
+    static const long long nt_min = [] {
+      const char* e = getenv("SMPQ_NT_MIN_MB");
+      return (e ? atoll(e) : 64LL) << 20;
+    }();
+    a.nt_store = (yq && (long long)limbs * M * cout >= nt_min) ? 1 : 0;
+  }
   hipStream_t s = (hipStream_t)stream;
   if (tile_cfg < 0) {
     const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
@@ -1143,7 +1149,8 @@ extern "C" int smpq_maxpool_limbs(const int8_t* x, int n, int h, int w, int c, i
   const int ho = (h + 2 - 3) / 2 + 1, wo = (w + 2 - 3) / 2 + 1;
   const long long iplane = (long long)n * h * w * c, oplane = (long long)n * ho * wo * c;
   const long long total = (long long)n * ho * wo * (c / 16);
-  const dim3 grid((unsigned)std::min<long long>((total + 255) / 256, 65535));
+  if (total > 0x7fffff00LL) return fail(SMPQ_E_SHAPE, "smpq_maxpool_limbs: too many outputs");
+  const dim3 grid((unsigned)((total + 255) / 256));
   hipStream_t s = (hipStream_t)stream;
   switch (limbs) {
     case 1: hipLaunchKernelGGL(maxpool_limbs_kernel<1>, grid, dim3(256), 0, s, x, n, h, w, c, ho, wo, iplane, out, oplane); break;

@@ -28,6 +28,7 @@ struct ConvArgs {
   int n, h, w, cin, cout, kh, kw, stride, pad, ho, wo;
   int M, K, ksteps, cchunks;
   int relu, has_offset;
+  int nt_store;  // limb-plane output stores with the non-temporal policy (outputs too big for the MALL)
   float inv_qmax;
   int s2d;  // space-to-depth stem (smpq_stem_conv_s2d_q): cin 16, 4 x 4 taps, K step = one tap row
 };
@@ -62,5 +63,56 @@ void glds_cfg_info(int cfg, int* bm, int* bn, int* threads);
 int glds_cfg_bk(int cfg);
 bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs);
 int launch_glds(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s);
+
+// The 4 codes (channels 0..3) held by one dword per limb plane, w[l] = the 4 balanced digits of
+// limb l: q = sum_l d_l 256^l. With u_l = d_l + 128 (byte ^ 0x80) for the low limbs,
+// q = sext24(u0 | u1 << 8 | d2 << 16) - 0x8080 (L = 3), sext16(u0 | d1 << 8) - 0x80 (L = 2).
+template <int L>
+__device__ __forceinline__ void decode4(const unsigned* w, int* q) {
+  if constexpr (L == 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) q[r] = __builtin_amdgcn_sbfe((int)w[0], 8 * r, 8);
+  } else if constexpr (L == 2) {
+    const unsigned x0 = w[0] ^ 0x80808080u;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const unsigned b = __builtin_amdgcn_perm(w[1], x0, (unsigned)r | ((unsigned)(r + 4) << 8) | 0x0c0c0000u);
+      q[r] = __builtin_amdgcn_sbfe((int)b, 0, 16) - 0x80;
+    }
+  } else {
+    const unsigned x0 = w[0] ^ 0x80808080u, x1 = w[1] ^ 0x80808080u;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // [u0(2h), u1(2h), u0(2h+1), u1(2h+1)]
+      const unsigned a = __builtin_amdgcn_perm(x1, x0, h == 0 ? 0x05010400u : 0x07030602u);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int r = 2 * h + e;
+        const unsigned sel = (e == 0 ? 0x0100u : 0x0302u) | ((unsigned)(4 + r) << 16) | 0x0c000000u;
+        const unsigned b = __builtin_amdgcn_perm(w[2], a, sel);
+        q[r] = __mul24((int)b, 1) - 0x8080;  // 24-bit operand: sign from bit 23 (v_mad_i32_i24)
+      }
+    }
+  }
+}
+
+// The digit dwords of 4 clamped codes (inverse of decode4): with Q = q + 0x8080 (L = 3) / q + 0x80
+// (L = 2), digit l of q is byte l of Q, xor 0x80 for every limb below the top one.
+template <int L>
+__device__ __forceinline__ void encode4(const int* q, unsigned* w) {
+  constexpr int bias = L == 3 ? 0x8080 : (L == 2 ? 0x80 : 0);
+  const unsigned Q0 = (unsigned)(q[0] + bias), Q1 = (unsigned)(q[1] + bias), Q2 = (unsigned)(q[2] + bias),
+                 Q3 = (unsigned)(q[3] + bias);
+  const unsigned a = __builtin_amdgcn_perm(Q1, Q0, 0x05010400u);  // [Q0.b0, Q1.b0, Q0.b1, Q1.b1]
+  const unsigned b = __builtin_amdgcn_perm(Q3, Q2, 0x05010400u);
+  constexpr unsigned flip = 0x80808080u;
+  w[0] = __builtin_amdgcn_perm(b, a, 0x05040100u) ^ (L > 1 ? flip : 0u);
+  if constexpr (L >= 2) w[1] = __builtin_amdgcn_perm(b, a, 0x07060302u) ^ (L > 2 ? flip : 0u);
+  if constexpr (L >= 3) {
+    const unsigned c = __builtin_amdgcn_perm(Q1, Q0, 0x07030602u);  // [Q0.b2, Q1.b2, Q0.b3, Q1.b3]
+    const unsigned d = __builtin_amdgcn_perm(Q3, Q2, 0x07030602u);
+    w[2] = __builtin_amdgcn_perm(d, c, 0x05040100u);
+  }
+}
 
 }  // namespace smpq

@@ -40,6 +40,20 @@ constexpr int kAblate = SMPQ_DIAG_ABLATE;
 constexpr unsigned kOOB = 0x80000000u;  // a buffer offset past every range we build (< 2^31 B)
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
+// 16-B store with the default (temporal) or the non-temporal cache policy (gfx950 CPol nt), as
+// inline asm that ends with one wait state: a VMEM store of more than 8 bytes must not have its data
+// VGPRs overwritten by the very next instruction, and ROCm 7.2's gfx950 hazard recognizer does not
+// always separate them (observed: dword 0 of a limb-plane store intermittently replaced by the
+// register's next value when a v_mov to it directly followed the store). nt is wave-uniform.
+__device__ __forceinline__ void store_limbs16(v4u v, v4i rs, unsigned off, unsigned soff, bool nt) {
+  if (nt)
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen nt\n\ts_nop 0" ::"v"(v), "v"(off), "s"(rs), "s"(soff)
+                 : "memory");
+  else
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 0" ::"v"(v), "v"(off), "s"(rs), "s"(soff)
+                 : "memory");
+}
+
 // byte offset of an fp32 element offset (kOOB stays out of range: 4 * kOOB would wrap to 0)
 __device__ __forceinline__ unsigned f32_off(unsigned e) { return e == kOOB ? kOOB : 4u * e; }
 
@@ -125,57 +139,6 @@ __device__ __forceinline__ unsigned pack_bytes(int b0, int b1, int b2, int b3, i
 }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
-
-// The 4 codes (channels 0..3) held by one dword per limb plane, w[l] = the 4 balanced digits of
-// limb l: q = sum_l d_l 256^l. With u_l = d_l + 128 (byte ^ 0x80) for the low limbs,
-// q = sext24(u0 | u1 << 8 | d2 << 16) - 0x8080 (L = 3), sext16(u0 | d1 << 8) - 0x80 (L = 2).
-template <int L>
-__device__ __forceinline__ void decode4(const unsigned* w, int* q) {
-  if constexpr (L == 1) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) q[r] = __builtin_amdgcn_sbfe((int)w[0], 8 * r, 8);
-  } else if constexpr (L == 2) {
-    const unsigned x0 = w[0] ^ 0x80808080u;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const unsigned b = __builtin_amdgcn_perm(w[1], x0, (unsigned)r | ((unsigned)(r + 4) << 8) | 0x0c0c0000u);
-      q[r] = __builtin_amdgcn_sbfe((int)b, 0, 16) - 0x80;
-    }
-  } else {
-    const unsigned x0 = w[0] ^ 0x80808080u, x1 = w[1] ^ 0x80808080u;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      // [u0(2h), u1(2h), u0(2h+1), u1(2h+1)]
-      const unsigned a = __builtin_amdgcn_perm(x1, x0, h == 0 ? 0x05010400u : 0x07030602u);
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int r = 2 * h + e;
-        const unsigned sel = (e == 0 ? 0x0100u : 0x0302u) | ((unsigned)(4 + r) << 16) | 0x0c000000u;
-        const unsigned b = __builtin_amdgcn_perm(w[2], a, sel);
-        q[r] = __mul24((int)b, 1) - 0x8080;  // 24-bit operand: sign from bit 23 (v_mad_i32_i24)
-      }
-    }
-  }
-}
-
-// The digit dwords of 4 clamped codes (inverse of decode4): with Q = q + 0x8080 (L = 3) / q + 0x80
-// (L = 2), digit l of q is byte l of Q, xor 0x80 for every limb below the top one.
-template <int L>
-__device__ __forceinline__ void encode4(const int* q, unsigned* w) {
-  constexpr int bias = L == 3 ? 0x8080 : (L == 2 ? 0x80 : 0);
-  const unsigned Q0 = (unsigned)(q[0] + bias), Q1 = (unsigned)(q[1] + bias), Q2 = (unsigned)(q[2] + bias),
-                 Q3 = (unsigned)(q[3] + bias);
-  const unsigned a = __builtin_amdgcn_perm(Q1, Q0, 0x05010400u);  // [Q0.b0, Q1.b0, Q0.b1, Q1.b1]
-  const unsigned b = __builtin_amdgcn_perm(Q3, Q2, 0x05010400u);
-  constexpr unsigned flip = 0x80808080u;
-  w[0] = __builtin_amdgcn_perm(b, a, 0x05040100u) ^ (L > 1 ? flip : 0u);
-  if constexpr (L >= 2) w[1] = __builtin_amdgcn_perm(b, a, 0x07060302u) ^ (L > 2 ? flip : 0u);
-  if constexpr (L >= 3) {
-    const unsigned c = __builtin_amdgcn_perm(Q1, Q0, 0x07030602u);  // [Q0.b2, Q1.b2, Q0.b3, Q1.b3]
-    const unsigned d = __builtin_amdgcn_perm(Q3, Q2, 0x07030602u);
-    w[2] = __builtin_amdgcn_perm(d, c, 0x05040100u);
-  }
-}
 
 }  // namespace
 
@@ -428,11 +391,6 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
                                                                                   (unsigned)((long long)l * oplane), 0);
   }
 
-  // per-pixel activation scale (per-image range): loaded now, used in the epilogue
-  float rscale[WP];
-#pragma unroll
-  for (int j = 0; j < WP; ++j) rscale[j] = mok[j] ? a.x_absmax[mrow[j] / hw_out] * a.inv_qmax : 0.f;
-
   // DMA pieces this wave issues per K step (wave-uniform): the counted vmcnt below
   int ppw = 0;
 #pragma unroll
@@ -597,6 +555,9 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
       }
     }
   }
+  float rscale[WP];
+#pragma unroll
+  for (int j = 0; j < WP; ++j) rscale[j] = mok[j] ? a.x_absmax[mrow[j] / hw_out] * a.inv_qmax : 0.f;
   // residual limb planes -> codes, all at once (one LDS wait instead of one per block)
   int rqv[WC][WP][4];
   if (a.res_q) {
@@ -671,20 +632,22 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
         for (int r = 0; r < 4; ++r) o[i][j][r] = fmaxf(o[i][j][r], 0.f);
   }
   if (a.y) {
-    const auto yrs = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)(4 * oplane), 0x00020000);
+    const v4i yrs4 = make_rsrc(a.y, 4LL * oplane);
 #pragma unroll
     for (int i = 0; i < WC; ++i)
 #pragma unroll
       for (int j = 0; j < WP; ++j) {
         const v4u v = {__float_as_uint(o[i][j][0]), __float_as_uint(o[i][j][1]), __float_as_uint(o[i][j][2]),
                        __float_as_uint(o[i][j][3])};
-        __builtin_amdgcn_raw_buffer_store_b128(v, yrs, f32_off(ooff[i][j]), 0, 0);
+        store_limbs16(v, yrs4, f32_off(ooff[i][j]), 0u, false);
       }
   }
   constexpr float qmax = act_qmax<L>();
   if (a.yq) {
     // fused quantizer of the next conv's input (static range): one dword per limb plane
     const auto qrs = __builtin_amdgcn_make_buffer_rsrc(a.yq, 0, (int)(L * oplane), 0x00020000);
+    const v4i qrs4 = make_rsrc(a.yq, (long long)L * oplane);
+    const bool nt = __builtin_amdgcn_readfirstlane(a.nt_store) != 0;
     float vmax = 0.f;
     unsigned wq[WC][WP][L];
 #pragma unroll
@@ -714,8 +677,8 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
             unsigned w0 = wq[4 * q][j][l], w1 = wq[4 * q + 1][j][l], w2 = wq[4 * q + 2][j][l], w3 = wq[4 * q + 3][j][l];
             transpose4(w0, w1, w2, w3);
             if (!(kAblate & 2) || w0 == 0x12345679u)
-              __builtin_amdgcn_raw_buffer_store_b128(v4u{w0, w1, w2, w3}, qrs, qoff[q][j],
-                                                     (unsigned)((long long)l * oplane), 0);
+              store_limbs16(v4u{w0, w1, w2, w3}, qrs4, qoff[q][j],
+                            __builtin_amdgcn_readfirstlane((unsigned)((long long)l * oplane)), nt);
           }
     } else if (TR) {
       // stage the [L][BP][BC] tile in the operand area (every wave is past its last fragment
@@ -739,8 +702,8 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
           const bool ok = m0 + rt < a.M && n0 + 16 * c < a.cout;
           const unsigned off = ok ? (unsigned)((long long)(m0 + rt) * a.cout + n0 + 16 * c) : kOOB;
           if (!(kAblate & 2) || v.x == 0x12345679)
-            __builtin_amdgcn_raw_buffer_store_b128(v4u{(unsigned)v.x, (unsigned)v.y, (unsigned)v.z, (unsigned)v.w},
-                                                   qrs, off, (unsigned)((long long)l * oplane), 0);
+            store_limbs16(v4u{(unsigned)v.x, (unsigned)v.y, (unsigned)v.z, (unsigned)v.w}, qrs4, off,
+                          __builtin_amdgcn_readfirstlane((unsigned)((long long)l * oplane)), nt);
         }
       }
     } else {

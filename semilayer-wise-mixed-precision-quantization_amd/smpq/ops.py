@@ -413,9 +413,11 @@ def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, 
     cfg = _TUNED.get(key)
     if cfg is None and AUTOTUNE[0] and not torch.cuda.is_current_stream_capturing():
         best = None
-        for c in tile_configs():
-            if not _tile_fits(c, limbs, wlimbs, cin == 4, cout, cin, kh):
-                continue
+        cands = [c for c in tile_configs() if _tile_fits(c, limbs, wlimbs, cin == 4, cout, cin, kh)]
+        # the register-staged family only where no LDS-DMA config takes the shape (it is never the
+        # fastest on R50 shapes, and its epilogue showed intermittent limb-plane mismatches)
+        lds = [c for c in cands if tile_kind(c) in (TILE_LDS_DMA, TILE_LDS_DMA_K128)]
+        for c in (lds or cands):
             times = []
             try:
                 for rep in range(3):

@@ -24,6 +24,7 @@ SHAPES = [  # name, cin, cout, k, stride, hin, residual
     ("c1_256_64_56", 256, 64, 1, 1, 56, False),
     ("c2_64_64_56", 64, 64, 3, 1, 56, False),
     ("c3_64_256_56", 64, 256, 1, 1, 56, True),
+    ("ds_64_256_56", 64, 256, 1, 1, 56, False),
     ("c2_256_256_14", 256, 256, 3, 1, 14, False),
     ("c3_256_1024_14", 256, 1024, 1, 1, 14, True),
     ("c1_1024_256_14", 1024, 256, 1, 1, 14, False),
