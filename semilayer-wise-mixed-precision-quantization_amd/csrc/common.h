@@ -50,11 +50,11 @@ __device__ __forceinline__ int wave_sum_i(int v) {
   return v;
 }
 
-// 16-B global store followed by one wait state: on gfx950 a VMEM store of more than 8 bytes must
+// 16-B global store followed by two wait states (the gfx940-family count): on gfx950 a VMEM store of more than 8 bytes must
 // not have its data VGPRs rewritten by the next instruction, and ROCm 7.2's hazard recognizer does
 // not always keep them apart (conv_glds.hip store_limbs16 has the observed failure).
 __device__ __forceinline__ void st16(void* p, v4i v) {
-  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 0" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 // atomic max on a non-negative float stored as its bit pattern (monotone for v >= 0)

@@ -41,16 +41,16 @@ constexpr unsigned kOOB = 0x80000000u;  // a buffer offset past every range we b
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // 16-B store with the default (temporal) or the non-temporal cache policy (gfx950 CPol nt), as
-// inline asm that ends with one wait state: a VMEM store of more than 8 bytes must not have its data
+// inline asm that ends with two wait states (the gfx940-family count): a VMEM store of more than 8 bytes must not have its data
 // VGPRs overwritten by the very next instruction, and ROCm 7.2's gfx950 hazard recognizer does not
 // always separate them (observed: dword 0 of a limb-plane store intermittently replaced by the
 // register's next value when a v_mov to it directly followed the store). nt is wave-uniform.
 __device__ __forceinline__ void store_limbs16(v4u v, v4i rs, unsigned off, unsigned soff, bool nt) {
   if (nt)
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen nt\n\ts_nop 0" ::"v"(v), "v"(off), "s"(rs), "s"(soff)
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen nt\n\ts_nop 1" ::"v"(v), "v"(off), "s"(rs), "s"(soff)
                  : "memory");
   else
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 0" ::"v"(v), "v"(off), "s"(rs), "s"(soff)
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(off), "s"(rs), "s"(soff)
                  : "memory");
 }
 
@@ -152,6 +152,8 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
   case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
     SMPQ_VMW(1) SMPQ_VMW(2) SMPQ_VMW(3) SMPQ_VMW(4) SMPQ_VMW(5) SMPQ_VMW(6) SMPQ_VMW(7) SMPQ_VMW(8)
     SMPQ_VMW(9) SMPQ_VMW(10) SMPQ_VMW(11) SMPQ_VMW(12) SMPQ_VMW(13) SMPQ_VMW(14) SMPQ_VMW(15) SMPQ_VMW(16)
+    SMPQ_VMW(17) SMPQ_VMW(18) SMPQ_VMW(19) SMPQ_VMW(20) SMPQ_VMW(21) SMPQ_VMW(22) SMPQ_VMW(23) SMPQ_VMW(24)
+    SMPQ_VMW(25) SMPQ_VMW(26) SMPQ_VMW(27) SMPQ_VMW(28) SMPQ_VMW(29) SMPQ_VMW(30) SMPQ_VMW(31) SMPQ_VMW(32)
 #undef SMPQ_VMW
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
@@ -784,6 +786,13 @@ constexpr GldsCfg kGlds[] = {
     {2, 2, 4, 1, 2, 128},  // 19: as 9
     {1, 4, 4, 2, 2, 128},  // 20: as 4
     {2, 4, 4, 2, 2, 128},  // 21: as 13
+    // deeper DMA pipelines for the long-K 3x3 convs (latency of a K step's pieces hidden behind
+    // NST - 1 steps of MFMAs)
+    {2, 2, 4, 2, 4, 64},   // 22: as 2, 4 stages
+    {2, 2, 2, 2, 4, 64},   // 23: as 0, 4 stages
+    {1, 4, 4, 1, 4, 64},   // 24: as 3, 4 stages
+    {2, 2, 4, 2, 3, 128},  // 25: as 18, 3 stages
+    {2, 2, 2, 2, 3, 128},  // 26: as 16, 3 stages
 };
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
@@ -881,6 +890,11 @@ static int launch_cfg(int cfg, const ConvArgs& a, hipStream_t s) {
     case 19: return launch_one<L, LW, 2, 2, 4, 1, false, 2, 2, 128>(a, s);
     case 20: return launch_one<L, LW, 1, 4, 4, 2, false, 2, 2, 128>(a, s);
     case 21: return launch_one<L, LW, 2, 4, 4, 2, false, 2, 2, 128>(a, s);
+    case 22: return launch_one<L, LW, 2, 2, 4, 2, false, 4>(a, s);
+    case 23: return launch_one<L, LW, 2, 2, 2, 2, false, 4>(a, s);
+    case 24: return launch_one<L, LW, 1, 4, 4, 1, false, 4>(a, s);
+    case 25: return launch_one<L, LW, 2, 2, 4, 2, false, 3, 2, 128>(a, s);
+    case 26: return launch_one<L, LW, 2, 2, 2, 2, false, 3, 2, 128>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   }
 }

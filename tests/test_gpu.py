@@ -755,3 +755,24 @@ def test_tile_configs_deterministic(gpu, shape):
             y, q = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, tile_cfg=c, emit_range=rng,
                                 overflow=ovf, **kw)
             assert torch.equal(y, y0) and torch.equal(q, q0), (c, rep)
+
+
+def test_forward_independent_of_previous_input(gpu):
+    """A forward's result must not depend on what ran before it (stale memory or registers): the
+    static-range forward of x, then of x2, then of x again gives x's logits bit for bit, several
+    times over (a VMEM store-data hazard once left x2's limb-plane bytes in x's activations)."""
+    from smpq import engine
+    net = build_model(gpu, "resnet50", "r50_mixed")
+    x = torch.randn(6, 3, 224, 224, generator=torch.Generator().manual_seed(14)).to(gpu)
+    x2 = torch.randn(6, 3, 224, 224, generator=torch.Generator().manual_seed(15)).to(gpu)
+    use = engine.USE_GRAPH[0]
+    engine.USE_GRAPH[0] = False
+    try:
+        with torch.no_grad():
+            net(x)
+            e1 = net(x)
+            for _ in range(3):
+                net(x2)
+                assert torch.equal(net(x), e1)
+    finally:
+        engine.USE_GRAPH[0] = use

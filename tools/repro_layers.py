@@ -50,20 +50,38 @@ ops.stem_conv_s2d = stem_rec
 ops.maxpool_limbs = pool_rec
 engine.USE_GRAPH[0] = False
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+MODE = sys.argv[2] if len(sys.argv) > 2 else "static"   # "dynamic-first": first call (autotuning) vs second
 for it in range(N):
-    net = build_model(gpu, "resnet50", "r50_mixed")
-    x = torch.randn(6, 3, 224, 224, generator=torch.Generator().manual_seed(14)).to(gpu)
-    x2 = torch.randn(6, 3, 224, 224, generator=torch.Generator().manual_seed(15)).to(gpu)
-    with torch.no_grad():
-        net(x)
-        net(x)  # autotune outside the recorded runs
-        REC.clear()
-        e1 = net(x)
-        r1 = list(REC)
-        net(x2)
-        REC.clear()
-        e3 = net(x)
-        r3 = list(REC)
+    if MODE in ("dynamic-first", "dynamic-pair"):
+        engine.set_range_mode("dynamic")
+        if MODE == "dynamic-first":
+            ops._TUNED.clear()
+        net = build_model(gpu, "resnet18", "r18_u8")
+        x = torch.randn(64, 3, 224, 224, generator=torch.Generator().manual_seed(11)).to(gpu)
+        with torch.no_grad():
+            if MODE == "dynamic-pair":
+                net(x)
+            REC.clear()
+            e1 = net(x)
+            r1 = list(REC)
+            REC.clear()
+            e3 = net(x)
+            r3 = list(REC)
+        engine.set_range_mode("static")
+    else:
+        net = build_model(gpu, "resnet50", "r50_mixed")
+        x = torch.randn(6, 3, 224, 224, generator=torch.Generator().manual_seed(14)).to(gpu)
+        x2 = torch.randn(6, 3, 224, 224, generator=torch.Generator().manual_seed(15)).to(gpu)
+        with torch.no_grad():
+            net(x)
+            net(x)  # autotune outside the recorded runs
+            REC.clear()
+            e1 = net(x)
+            r1 = list(REC)
+            net(x2)
+            REC.clear()
+            e3 = net(x)
+            r3 = list(REC)
     torch.cuda.synchronize()
     diff = (e1 - e3).abs().amax(1).tolist()
     print("iter", it, "logits diff per image", [round(v, 5) for v in diff], "launches", len(r1), len(r3), flush=True)
