@@ -930,6 +930,8 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
   a.wplane = (long long)cout * a.K;
   a.relu = relu ? 1 : 0;
   a.has_offset = (offset && wlimbs == 1) ? 1 : 0;
+  fast_div_init(a.ho * a.wo, a.hw_mul, a.hw_shr);
+  fast_div_init(a.wo, a.wo_mul, a.wo_shr);
   {
     // outputs larger than this stream past the 256-MB MALL anyway: store them non-temporally
     static const long long nt_min = [] {
@@ -1121,6 +1123,8 @@ extern "C" int smpq_stem_conv_s2d_q(const int8_t* xq, const float* x_absmax, int
   a.wplane = (long long)cout * a.K;
   a.relu = relu ? 1 : 0;
   a.inv_qmax = 1.f / (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f));
+  fast_div_init(a.ho * a.wo, a.hw_mul, a.hw_shr);
+  fast_div_init(a.wo, a.wo_mul, a.wo_shr);
   if ((long long)n * a.ho * a.wo > 0x7fffffffLL) return fail(SMPQ_E_SHAPE, "smpq_stem_conv_s2d_q: tensor too large");
   return launch_glds(tile_cfg - kNumTileCfgs, limbs, wlimbs, a, (hipStream_t)stream);
 }

@@ -29,9 +29,26 @@ struct ConvArgs {
   int M, K, ksteps, cchunks;
   int relu, has_offset;
   int nt_store;  // limb-plane output stores with the non-temporal policy (outputs too big for the MALL)
+  // x / d = (x * mul) >> shr for 0 <= x < 2^31 (fast_div_init): output pixels per image, output
+  // width, and (set by the tile launcher) channel tiles
+  unsigned hw_mul, wo_mul, ntc_mul;
+  int hw_shr, wo_shr, ntc_shr;
   float inv_qmax;
   int s2d;  // space-to-depth stem (smpq_stem_conv_s2d_q): cin 16, 4 x 4 taps, K step = one tap row
 };
+
+// Division by a runtime constant d >= 1 for numerators in [0, 2^31): p = 31 + ceil(log2 d),
+// mul = ceil(2^p / d) (< 2^32), x / d == (x * mul) >> p. Two instructions instead of the ~20 of a
+// generic 32-bit division (the conv prologues decompose pixel indices with it).
+inline void fast_div_init(int d, unsigned& mul, int& shr) {
+  int l = 0;
+  while ((1LL << l) < (long long)d) ++l;
+  shr = 31 + l;
+  mul = (unsigned)(((1ULL << shr) + (unsigned long long)d - 1) / (unsigned long long)d);
+}
+__device__ __forceinline__ int fast_div(int x, unsigned mul, int shr) {
+  return (int)(((unsigned long long)(unsigned)x * mul) >> shr);
+}
 
 template <int L>
 __device__ __host__ constexpr float act_qmax() {

@@ -202,8 +202,9 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
   const int full = total & ~7;
   int t = blockIdx.x;
   if (t < full) t = (t & 7) * (full >> 3) + (t >> 3);
-  const int m0 = (t / ntc) * BP;
-  const int n0 = (t % ntc) * BC;
+  const int tq = fast_div(t, a.ntc_mul, a.ntc_shr);  // t / ntc
+  const int m0 = tq * BP;
+  const int n0 = (t - tq * ntc) * BC;
   const int hw_out = a.ho * a.wo;
 
   const v4i wrs = make_rsrc(a.codes, (long long)LW * a.wplane);
@@ -233,9 +234,9 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
     const int m = m0 + RPP * bj + prow;
     const int pchunk = pchunk_of(bj);
     if (p < APIECES && m < a.M) {
-      const int img = m / hw_out;
+      const int img = fast_div(m, a.hw_mul, a.hw_shr);
       const int rem = m - img * hw_out;
-      const int oh = rem / a.wo, ow = rem - (rem / a.wo) * a.wo;
+      const int oh = fast_div(rem, a.wo_mul, a.wo_shr), ow = rem - oh * a.wo;
       if constexpr (S2D) {
         aih[s] = oh - a.pad;
         aiw[s] = ow - a.pad + pchunk;  // this lane's tap column, fixed over the K steps
@@ -559,7 +560,7 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
   }
   float rscale[WP];
 #pragma unroll
-  for (int j = 0; j < WP; ++j) rscale[j] = mok[j] ? a.x_absmax[mrow[j] / hw_out] * a.inv_qmax : 0.f;
+  for (int j = 0; j < WP; ++j) rscale[j] = mok[j] ? a.x_absmax[fast_div(mrow[j], a.hw_mul, a.hw_shr)] * a.inv_qmax : 0.f;
   // residual limb planes -> codes, all at once (one LDS wait instead of one per block)
   int rqv[WC][WP][4];
   if (a.res_q) {
@@ -738,7 +739,7 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
     const int mfirst = m0 + wp * WP * 16;
     const int mlast = min(mfirst + WP * 16, a.M) - 1;
     if (mfirst <= mlast) {
-      const int img_lo = mfirst / hw_out, img_hi = mlast / hw_out;
+      const int img_lo = fast_div(mfirst, a.hw_mul, a.hw_shr), img_hi = fast_div(mlast, a.hw_mul, a.hw_shr);
       if (img_lo == img_hi) {
         float v = 0.f;
 #pragma unroll
@@ -748,7 +749,7 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
       } else if (lane < 16) {
 #pragma unroll
         for (int j = 0; j < WP; ++j)
-          if (mok[j] && pmax[j] > 0.f) atomic_max_nonneg(&a.y_absmax[mrow[j] / hw_out], pmax[j]);
+          if (mok[j] && pmax[j] > 0.f) atomic_max_nonneg(&a.y_absmax[fast_div(mrow[j], a.hw_mul, a.hw_shr)], pmax[j]);
       }
     }
   }
@@ -860,7 +861,9 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
       (void)hipGetLastError();  // do not leave the error for the next, unrelated launch to report
       return check_hip(attr, "qconv_glds_kernel LDS attribute");
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)(mt * nt)), dim3(64 * WAVES_C * WAVES_P), lds_bytes, stream, a);
+    ConvArgs b = a;
+    fast_div_init((int)nt, b.ntc_mul, b.ntc_shr);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(mt * nt)), dim3(64 * WAVES_C * WAVES_P), lds_bytes, stream, b);
     return check_hip(hipGetLastError(), "qconv_glds_kernel launch");
   }
 }
