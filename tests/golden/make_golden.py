@@ -335,13 +335,44 @@ def make_eval_golden(functions):
                         softmax_a=torch.cat(out_a).numpy(), softmax_b=torch.cat(out_b).numpy(), kl=kl)
 
 
+def make_grouping_golden(functions):
+    """The reference's semilayer bookkeeping (functions.py:151-184, 590-612) on seeded lists,
+    including the postponing phase's misaligned call (resnet50_main.py:417: a SUBSET of the rows
+    paired index-by-index with the full Δloss list) and Δloss exactly 0 (goes to the minus side)."""
+    rng = np.random.default_rng(5)
+    sizes = [7, 1, 12, 4, 9]
+    params, d = [], []
+    n = 0
+    for ln, sz in enumerate(sizes, start=1):
+        for c in range(sz):
+            params.append([ln // 2, ln % 2, ln, c, 8, 0, int(rng.choice([32, 8, 6])), n])
+            d.append([ln // 2, ln % 2, ln, c] + [float(v) for v in rng.choice([-1.5, -0.25, 0.0, 0.5, 2.0], 4)])
+            n += 1
+    sub = [r for r in params if r[6] == 32]  # the postponing phase's subset
+    out = {"params": np.array(params, dtype=np.int64), "d": np.array(d, dtype=np.float64)}
+    for name, rows in (("full", params), ("subset", sub)):
+        for index in (4, 5, 6, 7):
+            mi, pl = functions.make_divide_minusplusmodels([list(r) for r in rows], d, index)
+            out["%s_%d_minus" % (name, index)] = np.array(mi, dtype=np.int64).reshape(-1, 8)
+            out["%s_%d_plus" % (name, index)] = np.array(pl, dtype=np.int64).reshape(-1, 8)
+    sem = [[list(r) for r in params if r[2] == ln] for ln in range(1, len(sizes) + 1)]
+    orders = [[i, float(v)] for i, v in enumerate(rng.permutation(len(sizes)) * 0.1)]
+    out["orders"] = np.array(orders, dtype=np.float64)
+    out["quantizedlist"] = np.array(functions.make_quantizedlists(sem, [list(o) for o in orders]), dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, "grouping_golden.npz"), **out)
+
+
 def main():
     os.makedirs(PKG_DATA, exist_ok=True)
     functions, resnet = import_reference()
     if sys.argv[1:] == ["eval"]:
         make_eval_golden(functions)
         return
+    if sys.argv[1:] == ["grouping"]:
+        make_grouping_golden(functions)
+        return
     make_eval_golden(functions)
+    make_grouping_golden(functions)
     assigns = {"r50_mixed": reconstruct_r50_mixed(), "r18_u8": r18_uniform8(),
                "r34_4bit": r34_4bit_dominant()}
     save_assignment("r50_mixed", "resnet50", *assigns["r50_mixed"])

@@ -1,12 +1,13 @@
 """libsmpq on the host: ABI exports, the native host quantizer vs the reference's KAT vectors,
 and the drop-in functions API on CPU tensors (no GPU needed)."""
+import os
 import re
 
 import numpy as np
 import pytest
 import torch
 
-from conftest import REPO
+from conftest import GOLDEN, REPO
 from test_oracle_golden import kat_cases
 
 
@@ -84,3 +85,24 @@ def test_dropin_kldiv_has_no_cpu_fallback():
     p = [torch.softmax(torch.randn(5, 10), 1)]
     with pytest.raises(ValueError):
         functions.KLdiv(p, p)
+
+
+def test_dropin_grouping_matches_reference_golden():
+    """functions.make_divide_minusplusmodels / make_quantizedlists vs the reference's own outputs
+    (tests/golden/grouping_golden.npz, make_golden.py grouping), including the postponing phase's
+    subset-vs-full-Δloss index misalignment (resnet50_main.py:417) kept bug-compatible."""
+    import functions
+    z = np.load(os.path.join(GOLDEN, "grouping_golden.npz"), allow_pickle=False)
+    params = z["params"].tolist()
+    d = z["d"].tolist()
+    sub = [r for r in params if r[6] == 32]
+    for name, rows in (("full", params), ("subset", sub)):
+        for index in (4, 5, 6, 7):
+            mi, pl = functions.make_divide_minusplusmodels([list(r) for r in rows], d, index)
+            np.testing.assert_array_equal(np.array(mi, dtype=np.int64).reshape(-1, 8), z["%s_%d_minus" % (name, index)])
+            np.testing.assert_array_equal(np.array(pl, dtype=np.int64).reshape(-1, 8), z["%s_%d_plus" % (name, index)])
+    nl = int(z["params"][:, 2].max())
+    sem = [[list(r) for r in params if r[2] == ln] for ln in range(1, nl + 1)]
+    orders = [[int(o[0]), float(o[1])] for o in z["orders"]]
+    got = functions.make_quantizedlists(sem, orders)
+    np.testing.assert_array_equal(np.array(got, dtype=np.int64), z["quantizedlist"])
