@@ -10,6 +10,7 @@ from . import ops  # noqa: F401
 from .ops import get_act_limbs, set_act_limbs  # noqa: F401
 from .qconv import QConv2d, stats  # noqa: F401
 from .quant import channel_wise_quantizationperchan, quantize_layer_, quantize_wgt  # noqa: F401
+from .checkpoint import load_checkpoint, save_checkpoint  # noqa: F401
 
 __all__ = ["ops", "QConv2d", "stats", "quantize_wgt", "channel_wise_quantizationperchan",
-           "quantize_layer_", "set_act_limbs", "get_act_limbs"]
+           "quantize_layer_", "set_act_limbs", "get_act_limbs", "save_checkpoint", "load_checkpoint"]

@@ -106,3 +106,18 @@ def test_reference_pth_runs_exact_int8_path(gpu, tmp_path):
     # bound of test_gpu.LOGIT_RTOL[3] (2e-4 of max |logit|), and identical top-1
     assert (a - b).abs().max().item() <= 2e-4 * a.abs().max().item()
     assert torch.equal(a.argmax(1), b.argmax(1))
+
+
+def test_sidecar_shape_mismatch_is_loud(built_lib, tmp_path):
+    import json
+    import resnet
+    from smpq import checkpoint
+    net = _mixed_net(built_lib)
+    p = tmp_path / "bad.pth"
+    checkpoint.save_checkpoint(net, p)
+    torch.save(_plain(torch.load(p, weights_only=True)), p)
+    side = json.load(open(checkpoint.sidecar_path(p)))
+    side["convs"]["1"] = side["convs"]["1"][:-1]
+    json.dump(side, open(checkpoint.sidecar_path(p), "w"))
+    with pytest.raises(ValueError):
+        checkpoint.load_checkpoint(resnet.resnet18(), p, strict=False)
