@@ -55,11 +55,25 @@ typedef void* smpq_stream_t; /* hipStream_t */
 int smpq_abi_version(void);
 const char* smpq_last_error(void);
 
-/* Fake-quantize channels of w in place, bit-exactly as functions.py:25-43.
+/* Rounding semantics of functions.py:41 `t / scale` (scale a Python float), which depend on
+ * where the reference's tensor lives:
+ *   SMPQ_QSEM_CPU     torch on the CPU: IEEE fp32 division t / fp32(scale)
+ *   SMPQ_QSEM_DEVICE  torch on the GPU: t * fp32(1.0 / scale) (reciprocal of the double scale,
+ *                     rounded once; tests/golden/quant_kat_device.npz, produced by torch on an
+ *                     MI355X, pins it) */
+#define SMPQ_QSEM_CPU 0
+#define SMPQ_QSEM_DEVICE 1
+
+/* Fake-quantize channels of w in place, bit-exactly as functions.py:25-43 executes under
+ * `semantics` (SMPQ_QSEM_*).
  *   w          device fp32 [cout][k_elems] (one output channel per row)
  *   bits       device int8 [cout]; 0 leaves the channel untouched
  *   scale_out  device fp32 [cout]; receives fp32(scale) of the quantization applied
  *   status     device int32 [1], caller-zeroed; set to (first constant channel)+1 */
+int smpq_quantize_channels_ex(float* w, int cout, int k_elems, const int8_t* bits,
+                              float* scale_out, int32_t* status, int semantics, smpq_stream_t stream);
+
+/* smpq_quantize_channels_ex with SMPQ_QSEM_CPU (ABI v1 entry point, kept). */
 int smpq_quantize_channels(float* w, int cout, int k_elems, const int8_t* bits,
                            float* scale_out, int32_t* status, smpq_stream_t stream);
 
@@ -67,6 +81,10 @@ int smpq_quantize_channels(float* w, int cout, int k_elems, const int8_t* bits,
  * weight lives in host memory (the reference quantizes CPU tensors of fresh models, e.g.
  * functions.py:504-512 right after resnet.resnet50(...) at :528). Returns SMPQ_E_CONSTANT on
  * a constant channel (channels before it are already quantized, as in the reference loop). */
+int smpq_quantize_channels_host_ex(float* w, int cout, int k_elems, const int8_t* bits,
+                                   float* scale_out, int semantics);
+
+/* smpq_quantize_channels_host_ex with SMPQ_QSEM_CPU (ABI v1 entry point, kept). */
 int smpq_quantize_channels_host(float* w, int cout, int k_elems, const int8_t* bits,
                                 float* scale_out);
 
@@ -238,6 +256,22 @@ int smpq_softmax_xent(const float* logits, const int64_t* labels, int rows, int 
                       double* stats, float* row_ws, smpq_stream_t stream);
 int smpq_kl_rows(const float* p_ref, const float* p, int rows, int cols, double* stats, float* row_ws,
                  smpq_stream_t stream);
+
+/* ---- content fingerprints (cache validation; smpq/engine.py) ------------------------------------
+ * smpq_fingerprint: out[t] = sum_i w_i * (2i + 1) mod 2^64 over the nwords[t] 32-bit words of
+ *   tensor t (device pointers ptrs[t], a device array), for t < ntensors; the work is split into
+ *   nchunks chunks of smpq_fingerprint_chunk_words() words: chunk c covers tensor chunk_tensor[c]
+ *   from word chunk_word[c] (device arrays). out (device uint64 [ntensors]) is overwritten.
+ *   Any single-word change changes the fingerprint (odd multipliers are invertible mod 2^64).
+ * smpq_fingerprint_compare: *flag |= 1 if a[i] != b[i] for some i < n (device arrays).
+ * smpq_fingerprint_host: the same sum over host memory.
+ * Used to detect in-place writes through `.data` (functions.py:22, resnet50_main.py:191) that
+ * leave a Parameter's version counter unchanged. */
+long long smpq_fingerprint_chunk_words(void);
+int smpq_fingerprint(const void* const* ptrs, const int64_t* nwords, int ntensors, const int32_t* chunk_tensor,
+                     const int64_t* chunk_word, int nchunks, uint64_t* out, smpq_stream_t stream);
+int smpq_fingerprint_compare(const uint64_t* a, const uint64_t* b, int n, int32_t* flag, smpq_stream_t stream);
+uint64_t smpq_fingerprint_host(const void* p, int64_t nwords);
 
 /* Diagnostics: one v_mfma_i32_16x16x64_i8 with the kernel's fragment mapping.
  *   a [16][64] int8 row-major, b [16][64] int8 (b[col][k]), c [16][16] int32 row-major */

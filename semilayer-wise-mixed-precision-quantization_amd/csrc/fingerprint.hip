@@ -1,0 +1,100 @@
+// Content fingerprints of the tensors a cached forward depends on (conv weights, quantization
+// metadata, BatchNorm buffers), so that a change the host cannot see is still caught.
+//
+// The reference and its drivers rewrite weights in place (functions.py:22 writes
+// `tensor[i][:][:][:] = ...` into conv.weight.data; resnet50_main.py:191 assigns `.data`); writes
+// through `.data` do not bump a Parameter's version counter, so the engine's host-side key
+// (data_ptr, _version) misses them. The engine fingerprints those tensors on the device after
+// each forward (inside the captured graph) and compares against the fingerprint taken when its
+// caches were built; a mismatch is reported with the overflow flag it already reads once per
+// forward, and the result is recomputed from freshly packed weights.
+//
+// Fingerprint of a tensor of N 32-bit words w_i: sum_i w_i * (2i + 1) mod 2^64. Every odd
+// multiplier is invertible mod 2^64, so any change of a single word changes the sum; the sum is
+// order-independent (exact integer atomics), hence deterministic. Work is split into chunks of
+// kChunkWords words; chunk c belongs to tensor chunk_tensor[c] and starts at word chunk_word[c].
+// HBM-bound: one read of every byte (R50: ~100 MB of fp32 weights, ~15-20 us).
+#include "common.h"
+
+namespace smpq {
+
+constexpr int kFpThreads = 256;
+constexpr long long kChunkWords = 16384;  // 64 KiB per block
+
+__global__ __launch_bounds__(kFpThreads) void fingerprint_kernel(const uint32_t* const* __restrict__ ptrs,
+                                                                   const long long* __restrict__ nwords,
+                                                                   const int* __restrict__ chunk_tensor,
+                                                                   const long long* __restrict__ chunk_word,
+                                                                   unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long part[kFpThreads / kWave];
+  const int c = blockIdx.x;
+  const int t = chunk_tensor[c];
+  const long long w0 = chunk_word[c];
+  const long long n = nwords[t];
+  const long long w1 = w0 + kChunkWords < n ? w0 + kChunkWords : n;
+  const uint32_t* p = ptrs[t];
+  unsigned long long acc = 0;
+  for (long long i = w0 + threadIdx.x; i < w1; i += kFpThreads)
+    acc += (unsigned long long)p[i] * (unsigned long long)(2 * i + 1);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, kWave);
+  const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  if (lane == 0) part[wid] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long s = 0;
+#pragma unroll
+    for (int i = 0; i < kFpThreads / kWave; ++i) s += part[i];
+    atomicAdd(out + t, s);
+  }
+}
+
+__global__ void fingerprint_zero_kernel(unsigned long long* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = 0ull;
+}
+
+__global__ void fingerprint_compare_kernel(const unsigned long long* __restrict__ a,
+                                           const unsigned long long* __restrict__ b, int n,
+                                           int32_t* __restrict__ flag) {
+  bool diff = false;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) diff |= a[i] != b[i];
+  if (__any(diff) && (threadIdx.x % kWave) == 0) atomicOr(flag, 1);
+}
+
+}  // namespace smpq
+
+using namespace smpq;
+
+extern "C" long long smpq_fingerprint_chunk_words(void) { return kChunkWords; }
+
+extern "C" int smpq_fingerprint(const void* const* ptrs, const int64_t* nwords, int ntensors,
+                                const int32_t* chunk_tensor, const int64_t* chunk_word, int nchunks,
+                                uint64_t* out, smpq_stream_t stream) {
+  if (!ptrs || !nwords || !chunk_tensor || !chunk_word || !out || ntensors <= 0 || nchunks <= 0)
+    return fail(SMPQ_E_INVALID, "smpq_fingerprint: bad arguments");
+  hipLaunchKernelGGL(fingerprint_zero_kernel, dim3((ntensors + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<unsigned long long*>(out), ntensors);
+  hipLaunchKernelGGL(fingerprint_kernel, dim3(nchunks), dim3(kFpThreads), 0, (hipStream_t)stream,
+                     reinterpret_cast<const uint32_t* const*>(ptrs), reinterpret_cast<const long long*>(nwords),
+                     chunk_tensor, reinterpret_cast<const long long*>(chunk_word),
+                     reinterpret_cast<unsigned long long*>(out));
+  return check_hip(hipGetLastError(), "fingerprint_kernel launch");
+}
+
+extern "C" int smpq_fingerprint_compare(const uint64_t* a, const uint64_t* b, int n, int32_t* flag,
+                                        smpq_stream_t stream) {
+  if (!a || !b || !flag || n <= 0) return fail(SMPQ_E_INVALID, "smpq_fingerprint_compare: bad arguments");
+  hipLaunchKernelGGL(fingerprint_compare_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const unsigned long long*>(a), reinterpret_cast<const unsigned long long*>(b),
+                     n, flag);
+  return check_hip(hipGetLastError(), "fingerprint_compare_kernel launch");
+}
+
+// Host twin (tests and CPU tensors): the same sum over one tensor's words.
+extern "C" uint64_t smpq_fingerprint_host(const void* p, int64_t nwords) {
+  const uint32_t* w = static_cast<const uint32_t*>(p);
+  unsigned long long acc = 0;
+  for (long long i = 0; i < nwords; ++i) acc += (unsigned long long)w[i] * (unsigned long long)(2 * i + 1);
+  return acc;
+}

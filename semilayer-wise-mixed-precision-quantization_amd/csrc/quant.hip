@@ -5,8 +5,15 @@
 //   scale   = (mx - mn) / (2^bit - 1)           IEEE double   (functions.py:39)
 //   z       = round(mn / scale)                 half-even      (functions.py:40)
 //   q       = (rne(t / f32(scale) + f32(z)) - f32(z)) * f32(scale)   fp32 ops (functions.py:41)
-// `t / f32(scale)` is a correctly rounded fp32 division (torch CPU divides; it does not
-// multiply by a reciprocal), so the device code uses __fdiv_rn and FP contraction is off.
+// What `t / scale` (scale a Python float) rounds to depends on where the reference's tensor lives:
+//   SMPQ_QSEM_CPU     torch CPU: a correctly rounded fp32 division t / f32(scale) (__fdiv_rn);
+//   SMPQ_QSEM_DEVICE  torch on the GPU: t * f32(1.0 / scale), a multiply by the reciprocal of the
+//                     DOUBLE scale rounded once to fp32 (ATen's tensor-by-scalar division on
+//                     device; pinned by tests/golden/quant_kat_device.npz, which torch itself
+//                     produced on an MI355X: 2 of the 69 KAT channels round differently there).
+// The reference's drivers quantize channels of a model already moved to the GPU
+// (functions.py:97 net.to(device) before resnet50_main.py:189-197), so device tensors default to
+// SMPQ_QSEM_DEVICE and host tensors to SMPQ_QSEM_CPU (smpq.quant). FP contraction is off.
 //
 // One workgroup per output channel: channels are at most 4608 elements (R50 layer4 conv2),
 // so a 256-thread block covers a channel in <= 18 iterations and the launch is a single
@@ -44,7 +51,7 @@ __device__ __forceinline__ void block_minmax(float& mn, float& mx, float* smem) 
 
 __global__ __launch_bounds__(kQThreads) void quantize_channels_kernel(
     float* __restrict__ w, int k, const int8_t* __restrict__ bits, float* __restrict__ scale_out,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ status, int semantics) {
   __shared__ float smem[2 * kQThreads / kWave];
   const int c = blockIdx.x;
   const int b = bits[c];
@@ -65,9 +72,12 @@ __global__ __launch_bounds__(kQThreads) void quantize_channels_kernel(
   const double zd = rint((double)mn / scale) + 0.0;  // Python round(): half-to-even; no -0
   const float s32 = (float)scale;
   const float z32 = (float)zd;
+  const float inv32 = (float)(1.0 / scale);
+  const bool dev = semantics == SMPQ_QSEM_DEVICE;
   for (int i = threadIdx.x; i < k; i += kQThreads) {
     const float t = row[i];
-    const float q = rintf(__fdiv_rn(t, s32) + z32) - z32;
+    const float d = dev ? __fmul_rn(t, inv32) : __fdiv_rn(t, s32);
+    const float q = rintf(d + z32) - z32;
     row[i] = __fmul_rn(q, s32);
   }
   if (threadIdx.x == 0) scale_out[c] = s32;
@@ -183,7 +193,7 @@ __global__ __launch_bounds__(kQThreads) void pack_weights_ex_kernel(
 // ------------------------------------------------------------------------------------------
 // host twin (native C++, same arithmetic)
 // ------------------------------------------------------------------------------------------
-static int quantize_row_host(float* row, int k, int b, float* s_out) {
+static int quantize_row_host(float* row, int k, int b, float* s_out, int semantics) {
   float mn = INFINITY, mx = -INFINITY;
   for (int i = 0; i < k; ++i) {
     mn = std::fmin(mn, row[i]);
@@ -194,8 +204,10 @@ static int quantize_row_host(float* row, int k, int b, float* s_out) {
   const double zd = std::nearbyint((double)mn / scale) + 0.0;
   const float s32 = (float)scale;
   const float z32 = (float)zd;
+  const float inv32 = (float)(1.0 / scale);
   for (int i = 0; i < k; ++i) {
-    const float d = row[i] / s32;  // fp32 IEEE division (contraction is off in this file)
+    // fp32 IEEE division, or the device's reciprocal multiply (contraction is off in this file)
+    const float d = semantics == SMPQ_QSEM_DEVICE ? row[i] * inv32 : row[i] / s32;
     const float q = std::nearbyintf(d + z32) - z32;
     row[i] = q * s32;
   }
@@ -207,31 +219,46 @@ static int quantize_row_host(float* row, int k, int b, float* s_out) {
 
 using namespace smpq;
 
-extern "C" int smpq_quantize_channels(float* w, int cout, int k_elems, const int8_t* bits,
-                                      float* scale_out, int32_t* status, smpq_stream_t stream) {
+extern "C" int smpq_quantize_channels_ex(float* w, int cout, int k_elems, const int8_t* bits,
+                                         float* scale_out, int32_t* status, int semantics,
+                                         smpq_stream_t stream) {
   if (!w || !bits || !scale_out || !status || cout <= 0 || k_elems <= 0)
     return fail(SMPQ_E_INVALID, "smpq_quantize_channels: bad arguments");
+  if (semantics != SMPQ_QSEM_CPU && semantics != SMPQ_QSEM_DEVICE)
+    return fail(SMPQ_E_INVALID, "smpq_quantize_channels: semantics must be SMPQ_QSEM_CPU or SMPQ_QSEM_DEVICE");
   hipLaunchKernelGGL(quantize_channels_kernel, dim3(cout), dim3(kQThreads), 0,
-                     (hipStream_t)stream, w, k_elems, bits, scale_out, status);
+                     (hipStream_t)stream, w, k_elems, bits, scale_out, status, semantics);
   return check_hip(hipGetLastError(), "quantize_channels_kernel launch");
 }
 
-extern "C" int smpq_quantize_channels_host(float* w, int cout, int k_elems, const int8_t* bits,
-                                           float* scale_out) {
+extern "C" int smpq_quantize_channels(float* w, int cout, int k_elems, const int8_t* bits,
+                                      float* scale_out, int32_t* status, smpq_stream_t stream) {
+  return smpq_quantize_channels_ex(w, cout, k_elems, bits, scale_out, status, SMPQ_QSEM_CPU, stream);
+}
+
+extern "C" int smpq_quantize_channels_host_ex(float* w, int cout, int k_elems, const int8_t* bits,
+                                              float* scale_out, int semantics) {
   if (!w || !bits || cout <= 0 || k_elems <= 0)
     return fail(SMPQ_E_INVALID, "smpq_quantize_channels_host: bad arguments");
+  if (semantics != SMPQ_QSEM_CPU && semantics != SMPQ_QSEM_DEVICE)
+    return fail(SMPQ_E_INVALID, "smpq_quantize_channels_host: semantics must be SMPQ_QSEM_CPU or SMPQ_QSEM_DEVICE");
   for (int c = 0; c < cout; ++c) {
     const int b = bits[c];
     if (b <= 0) continue;
     if (b > 30) return fail(SMPQ_E_BITS, "smpq_quantize_channels_host: bit > 30");
     float* row = w + (size_t)c * k_elems;
     float s32 = 0.f;
-    const int rc = quantize_row_host(row, k_elems, b, &s32);
+    const int rc = quantize_row_host(row, k_elems, b, &s32, semantics);
     if (rc != SMPQ_OK)
       return fail(rc, "float division by zero (constant channel " + std::to_string(c) + ")");
     if (scale_out) scale_out[c] = s32;
   }
   return SMPQ_OK;
+}
+
+extern "C" int smpq_quantize_channels_host(float* w, int cout, int k_elems, const int8_t* bits,
+                                           float* scale_out) {
+  return smpq_quantize_channels_host_ex(w, cout, k_elems, bits, scale_out, SMPQ_QSEM_CPU);
 }
 
 extern "C" int smpq_pack_weights(const float* w, int cout, int cin, int kh, int kw,

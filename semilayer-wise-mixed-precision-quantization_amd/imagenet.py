@@ -2,12 +2,15 @@
 
 The reference builds ``ImageFolder('./hogehoge/val')`` with Resize(256)/CenterCrop(224)/
 Normalize and a DataLoader(batch_size=256, num_workers=16, pin_memory=True). That needs
-torchvision and the ImageNet files; when either is missing (as on the build and GPU boxes)
-this module serves a deterministic synthetic stand-in of the same shape: N(0,1) 224x224
-images (comparable to normalized ImageNet) with seeded labels, ``SMPQ_SYNTH_IMAGES`` images
-(default 1024) in batches of ``SMPQ_BATCH`` (default 256).
+torchvision and the ImageNet files. Like the reference, a missing dataset is an error: a search
+run on random images would produce meaningless accuracies and KL orderings. A deterministic
+synthetic stand-in of the same shape (N(0,1) 224x224 images, comparable to normalized ImageNet,
+with seeded labels; ``SMPQ_SYNTH_IMAGES`` images, default 1024, in batches of ``SMPQ_BATCH``,
+default 256) is served only on explicit opt-in, ``SMPQ_SYNTHETIC=1`` (the build and GPU boxes
+have neither torchvision nor ImageNet), and announces itself on stderr.
 """
 import os
+import sys
 
 import torch
 
@@ -40,7 +43,9 @@ def _real_loader():
     return torch.utils.data.DataLoader(ds, batch_size=BATCH, shuffle=False, num_workers=16, pin_memory=True)
 
 
-try:
-    val_loader = _real_loader()
-except Exception:  # torchvision or the dataset absent
+if os.environ.get("SMPQ_SYNTHETIC", "0") == "1":
+    print("smpq imagenet: SMPQ_SYNTHETIC=1 -> synthetic N(0,1) val_loader (%s images), not ImageNet"
+          % os.environ.get("SMPQ_SYNTH_IMAGES", "1024"), file=sys.stderr)
     val_loader = SyntheticImageNet(int(os.environ.get("SMPQ_SYNTH_IMAGES", "1024")), BATCH)
+else:
+    val_loader = _real_loader()  # raises like the reference when torchvision / the dataset is absent

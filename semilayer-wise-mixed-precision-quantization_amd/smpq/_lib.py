@@ -37,6 +37,8 @@ _PROTOS = {
     "smpq_last_error": (ctypes.c_char_p, []),
     "smpq_quantize_channels": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp]),
     "smpq_quantize_channels_host": (_i, [_vp, _i, _i, _vp, _vp]),
+    "smpq_quantize_channels_ex": (_i, [_vp, _i, _i, _vp, _vp, _vp, _i, _vp]),
+    "smpq_quantize_channels_host_ex": (_i, [_vp, _i, _i, _vp, _vp, _i]),
     "smpq_pack_weights": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "smpq_act_absmax": (_i, [_vp, _i, _i64, _vp, _vp]),
     "smpq_act_quantize": (_i, [_vp, _i, _i64, _vp, _i, _vp, _vp]),
@@ -62,6 +64,10 @@ _PROTOS = {
     "smpq_debug_mfma_i8": (_i, [_vp, _vp, _vp, _vp]),
     "smpq_softmax_xent": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp]),
     "smpq_kl_rows": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp]),
+    "smpq_fingerprint_chunk_words": (ctypes.c_longlong, []),
+    "smpq_fingerprint": (_i, [_vp, _vp, _i, _vp, _vp, _i, _vp, _vp]),
+    "smpq_fingerprint_compare": (_i, [_vp, _vp, _i, _vp, _vp]),
+    "smpq_fingerprint_host": (ctypes.c_uint64, [_vp, _i64]),
 }
 
 EXPORTED_SYMBOLS = tuple(_PROTOS)

@@ -51,8 +51,9 @@ def addressable_convs(net):
     return out
 
 
-def apply_assignment(net, assign):
-    """Fake-quantize ``net`` per channel chain; one launch per (conv, chain step)."""
+def apply_assignment(net, assign, semantics=None):
+    """Fake-quantize ``net`` per channel chain; one launch per (conv, chain step). ``semantics``:
+    the rounding of functions.py:41 (ops.set_quant_semantics; None = the process setting)."""
     if isinstance(assign, str):
         assign = load_assignment(assign)
     lnum, cnum, chain = assign["lnum"], assign["cnum"], assign["chain"]
@@ -65,7 +66,7 @@ def apply_assignment(net, assign):
             bits = np.zeros(conv.out_channels, dtype=np.int64)
             bits[cnum[rows]] = chain[rows, step]
             if (bits > 0).any():
-                quantize_layer_(conv, bits)
+                quantize_layer_(conv, bits, semantics=semantics)
     return net
 
 

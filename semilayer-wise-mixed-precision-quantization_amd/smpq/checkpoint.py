@@ -8,8 +8,11 @@ only: the bit-widths are implicit in the values. Our QConv2d keeps ``qbits``/``q
 the other two cases:
 
 * ``save_checkpoint`` writes the state dict plus ``<path>.bits.json``, the per-channel bit
-  assignment in the reference's own vocabulary (lnum -> per-channel bits, 0 = never quantized),
-  readable without torch by the search drivers' bookkeeping;
+  assignment in the reference's own vocabulary (lnum -> per-channel bits, 0 = never quantized)
+  and the exact fp32 step of every channel (its IEEE bit pattern in hex), readable without torch
+  by the search drivers' bookkeeping. By default (``plain=True``) the ``.pth`` holds exactly the
+  reference's keys (no ``qbits``/``qstep``), so the reference's and torchvision's
+  ``load_state_dict(strict=True)`` accept it; the sidecar restores the metadata bitwise;
 * ``load_checkpoint`` / ``infer_quant_`` recover the metadata of a reference-written ``.pth``
   (no ``qbits``/``qstep`` keys): per channel, the smallest bit-width b whose re-quantization
   (functions.py:25-43 restated on the native library) leaves the channel bitwise unchanged is
@@ -43,23 +46,59 @@ def bit_assignment(net):
     return out
 
 
-def save_checkpoint(net, path):
-    """``torch.save(net.state_dict(), path)`` + ``<path>.bits.json``."""
-    torch.save(net.state_dict(), path)
-    side = {"format": "smpq-bits/1", "convs": {str(k): v for k, v in bit_assignment(net).items()}}
+META_KEYS = (".qbits", ".qstep")
+
+
+def plain_state_dict(net):
+    """``net.state_dict()`` without the quantization metadata buffers: the reference's keys only."""
+    return {k: v for k, v in net.state_dict().items() if not k.endswith(META_KEYS)}
+
+
+def step_assignment(net):
+    """{lnum: [fp32 step per output channel as its IEEE bit pattern, 8 hex digits]}."""
+    out = {}
+    for ln, conv in enumerate(addressable_convs(net), start=1):
+        bits = conv.qstep.detach().cpu().contiguous().view(torch.int32).numpy().astype(np.uint32)
+        out[ln] = ["%08x" % int(b) for b in bits]
+    return out
+
+
+def save_checkpoint(net, path, plain=True):
+    """``torch.save(net.state_dict(), path)`` + ``<path>.bits.json`` (bits + exact steps). With
+    ``plain`` the .pth carries the reference's keys only (loadable with strict=True by the
+    reference's / torchvision's ResNet); otherwise it also keeps the qbits/qstep buffers."""
+    torch.save(plain_state_dict(net) if plain else net.state_dict(), path)
+    side = {"format": "smpq-bits/2", "convs": {str(k): v for k, v in bit_assignment(net).items()},
+            "steps": {str(k): v for k, v in step_assignment(net).items()}}
     with open(sidecar_path(path), "w") as f:
         json.dump(side, f)
 
 
-def read_sidecar(path):
+def _read_sidecar_full(path):
     p = sidecar_path(path)
     if not os.path.exists(p):
-        return None
+        return None, None
     with open(p) as f:
         side = json.load(f)
-    if side.get("format") != "smpq-bits/1":
-        raise ValueError("%s: unknown sidecar format %r" % (p, side.get("format")))
-    return {int(k): np.asarray(v, dtype=np.int64) for k, v in side["convs"].items()}
+    fmt = side.get("format")
+    if fmt not in ("smpq-bits/1", "smpq-bits/2"):
+        raise ValueError("%s: unknown sidecar format %r" % (p, fmt))
+    bits = {int(k): np.asarray(v, dtype=np.int64) for k, v in side["convs"].items()}
+    steps = None
+    if fmt == "smpq-bits/2":
+        steps = {int(k): np.array([int(h, 16) for h in v], dtype=np.uint32).view(np.float32)
+                 for k, v in side["steps"].items()}
+    return bits, steps
+
+
+def read_sidecar(path):
+    """{lnum: int array of bits per channel} from ``<path>.bits.json``, or None."""
+    return _read_sidecar_full(path)[0]
+
+
+def read_sidecar_steps(path):
+    """{lnum: fp32 array of exact steps per channel} (format smpq-bits/2), or None."""
+    return _read_sidecar_full(path)[1]
 
 
 def infer_quant_(conv, allowed=None):
@@ -81,12 +120,18 @@ def infer_quant_(conv, allowed=None):
             todo &= np.asarray(allowed) == b
         if not todo.any():
             continue
-        work = w2d.clone()
-        step = ops.quantize_channels_(work, np.where(todo, b, 0))
-        same = (work == w2d).all(dim=1).cpu().numpy() & todo
-        found[same] = b
-        sel = torch.from_numpy(np.nonzero(same)[0]).to(steps.device)
-        steps[sel] = step.reshape(-1).to(steps.device)[sel]
+        # the channel may have been written by torch on the CPU or on the GPU (functions.py:41
+        # rounds differently there, ops.QSEM): either re-quantization that is a fixed point counts
+        for sem in ("cpu", "device"):
+            todo_s = todo & (found == 0)
+            if not todo_s.any():
+                break
+            work = w2d.clone()
+            step = ops.quantize_channels_(work, np.where(todo_s, b, 0), semantics=sem)
+            same = (work == w2d).all(dim=1).cpu().numpy() & todo_s
+            found[same] = b
+            sel = torch.from_numpy(np.nonzero(same)[0]).to(steps.device)
+            steps[sel] = step.reshape(-1).to(steps.device)[sel]
     # Re-quantization is not always idempotent (the min/max of a quantized channel round to a
     # grid shifted by an ulp): the rest get a direct grid search on the values
     lo_b = None if allowed is None else np.asarray(allowed)
@@ -125,13 +170,28 @@ def _grid_search(v, bits):
     return None
 
 
+def _strict_ok(net, state):
+    """strict=True for a plain (reference-format) state dict: only the metadata buffers, which the
+    QConv2d loader tolerates as missing, may be absent."""
+    want = set(net.state_dict())
+    missing = {k for k in want - set(state) if not k.endswith(META_KEYS)}
+    unexpected = set(state) - want
+    if missing or unexpected:
+        raise RuntimeError("Error(s) in loading state_dict: missing keys %s, unexpected keys %s"
+                           % (sorted(missing)[:8], sorted(unexpected)[:8]))
+
+
 def load_checkpoint(net, path, map_location="cpu", strict=True):
-    """``net.load_state_dict(torch.load(path))`` with a safe loader, then recover missing
-    quantization metadata (sidecar-guided when ``<path>.bits.json`` exists). Returns
+    """``net.load_state_dict(torch.load(path))`` with a safe loader, then restore the quantization
+    metadata: exactly from a smpq-bits/2 sidecar (bits + fp32 steps), else recovered from the
+    values (sidecar-guided when a smpq-bits/1 ``<path>.bits.json`` exists). Returns
     {lnum: bits per channel} after loading."""
     state = torch.load(path, map_location=map_location, weights_only=True)
-    net.load_state_dict(state, strict=strict)
-    side = read_sidecar(path)
+    if strict:
+        _strict_ok(net, state)
+    net.load_state_dict(state, strict=False)
+    side, side_steps = _read_sidecar_full(path)
+    has_meta = any(k.endswith(".qbits") for k in state)
     for ln, conv in enumerate(addressable_convs(net), start=1):
         allowed = None
         if side is not None:
@@ -141,5 +201,12 @@ def load_checkpoint(net, path, map_location="cpu", strict=True):
             if len(allowed) != conv.out_channels:
                 raise ValueError("sidecar lnum %d: %d channels, conv has %d"
                                  % (ln, len(allowed), conv.out_channels))
+            if side_steps is not None and not has_meta:
+                st = side_steps.get(ln)
+                if st is None or len(st) != conv.out_channels:
+                    raise ValueError("sidecar lnum %d: steps missing or of the wrong length" % ln)
+                conv.clear_quant()
+                conv.record_quant_all(np.asarray(allowed), torch.from_numpy(st.copy()))
+                continue
         infer_quant_(conv, allowed)
     return bit_assignment(net)

@@ -26,11 +26,19 @@ Range modes (``set_range_mode``):
     block-internal tensors, no quantize pass). A value beyond its range sets an overflow flag
     and the forward is recomputed in dynamic mode, widening the ranges, so results are never
     silently clamped. Calibration is redone whenever a weight, BN buffer or the limb count changes.
+
+Cache validity: every cache (packed codes, folded BN, ranges, the captured graph) is keyed on the
+identity, data_ptr and ``_version`` of every parameter and buffer of the model (a replaced
+Parameter, ``load_state_dict(assign=True)`` or a swapped submodule is seen), and on device-side
+content fingerprints of the conv weights / metadata / BN tensors (smpq/fingerprint.py), checked
+after every forward: a write through ``.data`` (no version bump) is detected, the result is
+discarded and recomputed from freshly packed weights.
 """
 import torch
 import torch.nn.functional as F
 
 from . import ops
+from .fingerprint import Fingerprinter
 from .qconv import QConv2d, stats
 
 _MODE = ["static"]
@@ -51,6 +59,7 @@ def set_chunk(n):
     CHUNK[0] = max(1, int(n))
 stats.setdefault("calibrations", 0)
 stats.setdefault("overflow_reruns", 0)
+stats.setdefault("stale_reruns", 0)
 
 
 def set_range_mode(mode):
@@ -88,7 +97,7 @@ def _bn_key(bn):
     ts = [bn.running_mean, bn.running_var]
     if bn.affine:
         ts += [bn.weight, bn.bias]
-    return tuple((t.data_ptr(), t._version) for t in ts) + (bn.eps,)
+    return tuple((id(t), t.data_ptr(), t._version) for t in ts) + (bn.eps,)
 
 
 def conv_plan(conv, bn):
@@ -131,7 +140,8 @@ class Ctx:
         self.n, self.device = n, device
         self.ranges = ranges            # {id(conv): range} (static mode) or None
         self.record = {} if record else None
-        self.overflow = torch.zeros(1, dtype=torch.int32, device=device) if ranges else None
+        # [0] a value exceeded its static range, [1] cached weight content is stale (fingerprint)
+        self.overflow = torch.zeros(2, dtype=torch.int32, device=device) if ranges else None
         self._rt = cache if cache is not None else {}
 
     def range_tensor(self, conv):
@@ -321,34 +331,42 @@ def _forward(model, x, ctx):
     return model.fc(torch.cat(feats))
 
 
-def _sig_tensors(model):
-    """(tensors, convs) the calibrated ranges and the captured graph depend on, listed once per model:
-    every conv weight and quantization metadata buffer and every BN buffer/affine parameter (the
-    reference and its drivers change weights through .data / load_state_dict — same tensor
-    objects — and never replace submodules)."""
-    st = getattr(model, "_smpq_sig_tensors", None)
-    if st is None:
-        tensors, convs = [], []
-        for m in model.modules():
-            if isinstance(m, QConv2d):
-                tensors += [m.weight, m.qstep, m.qbits]
-                convs.append(m)
-            elif isinstance(m, torch.nn.BatchNorm2d):
-                tensors += [m.running_mean, m.running_var] + ([m.weight, m.bias] if m.affine else [])
-        st = (tensors, convs)
-        model._smpq_sig_tensors = st
-    return st
+def _fp_tensors(model):
+    """Tensors whose CONTENT the caches are built from: conv weights (+ bias) and quantization
+    metadata (packed codes, folded scales), BN buffers / affine parameters (folded shift)."""
+    out = []
+    for m in model.modules():
+        if isinstance(m, QConv2d):
+            out += [m.weight, m.qstep, m.qbits] + ([m.bias] if m.bias is not None else [])
+        elif isinstance(m, torch.nn.BatchNorm2d):
+            out += [m.running_mean, m.running_var] + ([m.weight, m.bias] if m.affine else [])
+    return [t.detach() for t in out]
 
 
 def _signature(model):
-    """Value key of everything the calibrated ranges and the captured graph depend on."""
-    tensors, convs = _sig_tensors(model)
-    return (ops.get_act_limbs(), HEADROOM, tuple((t.data_ptr(), t._version) for t in tensors),
-            tuple(m._meta_gen for m in convs))
+    """Host key of everything the calibrated ranges and the captured graph depend on: identity,
+    data_ptr and version of every parameter and buffer (walked afresh each call, so replaced
+    Parameters, load_state_dict(assign=True) and swapped submodules are seen), each conv's
+    metadata and content generations and the limb count."""
+    ts = tuple((id(t), t.data_ptr(), t._version) for t in model.parameters()) + \
+        tuple((id(t), t.data_ptr(), t._version) for t in model.buffers())
+    convs = tuple((id(m), m._meta_gen, m._content_gen) for m in model.modules() if isinstance(m, QConv2d))
+    return (ops.get_act_limbs(), HEADROOM, ts, convs)
+
+
+def _fresh_fingerprint(model, device):
+    """Invalidate the model's content-keyed caches (its weights are repacked and BN refolded from
+    their current values on the next use) and fingerprint the current content: caches built from
+    here on match it."""
+    for m in model.modules():
+        if isinstance(m, QConv2d):
+            m._content_gen += 1
+    return Fingerprinter(_fp_tensors(model), device)
 
 
 def calibrate(model, x):
     """Dynamic forward of ``x`` that (re)sets the per-layer static ranges; returns its logits."""
+    fp = _fresh_fingerprint(model, x.device)
     ctx = Ctx(x.shape[0], x.device, record=True)
     y = _forward(model, x, ctx)
     keys = list(ctx.record)
@@ -361,7 +379,7 @@ def calibrate(model, x):
             if old is not None and old[1] == _signature(model) and k in old[0]:
                 r = max(r, old[0][k])
             ranges[k] = r
-        model._smpq_ranges = (ranges, _signature(model), {})
+        model._smpq_ranges = (ranges, _signature(model), {}, fp)
     stats["calibrations"] += 1
     return y
 
@@ -369,6 +387,7 @@ def calibrate(model, x):
 def _static_eager(model, x, cal):
     ctx = Ctx(x.shape[0], x.device, ranges=cal[0], cache=cal[2])
     y = _forward(model, x, ctx)
+    cal[3].check(ctx.overflow[1:])
     return y, ctx.overflow
 
 
@@ -388,15 +407,16 @@ def _graph_forward(model, x, cal):
     if entry is None or entry[0] != key:
         model._smpq_graph = None
         y, ovf = _static_eager(model, x, cal)  # warm every cache outside the capture
-        if int(ovf.item()) != 0:
+        if any(ovf.tolist()):
             return y, ovf
         static_x = x.clone()
         g = torch.cuda.CUDAGraph()
         ctx = Ctx(x.shape[0], x.device, ranges=cal[0], cache=cal[2])
         torch.cuda.synchronize()
         with torch.cuda.graph(g):
-            ctx.overflow = torch.zeros(1, dtype=torch.int32, device=x.device)
+            ctx.overflow = torch.zeros(2, dtype=torch.int32, device=x.device)
             y_static = _forward(model, static_x, ctx)
+            cal[3].check(ctx.overflow[1:])
         model._smpq_graph = (key, g, static_x, ctx, y_static)
         stats["graph_captures"] += 1
         return y, ovf
@@ -408,10 +428,27 @@ def _graph_forward(model, x, cal):
     return y_static.clone(), ctx.overflow
 
 
+def _dynamic_forward(model, x, retried=False):
+    """Dynamic-range forward (batch-independent results); one host sync for the content check."""
+    sig = _signature(model)
+    st = getattr(model, "_smpq_dyn", None)
+    if st is None or st[0] != sig:
+        fp = _fresh_fingerprint(model, x.device)
+        model._smpq_dyn = st = (_signature(model), fp)
+    y = _forward(model, x, None)
+    flag = torch.zeros(1, dtype=torch.int32, device=x.device)
+    st[1].check(flag)
+    if int(flag.item()) == 0 or retried:
+        return y
+    stats["stale_reruns"] += 1
+    model._smpq_dyn = None
+    return _dynamic_forward(model, x, retried=True)
+
+
 def forward_fused(model, x):
     """Eval-mode forward of an smpq ResNet on the GPU; returns logits [n, num_classes]."""
     if _MODE[0] == "dynamic":
-        return _forward(model, x, None)
+        return _dynamic_forward(model, x)
     cal = getattr(model, "_smpq_ranges", None)
     if cal is None:
         return calibrate(model, x)
@@ -429,7 +466,10 @@ def forward_fused(model, x):
             y, ovf = _graph_forward(model, x, cal)
         else:
             y, ovf = _static_eager(model, x, cal)
-    if int(ovf.item()) == 0:  # one sync: results are never silently clamped
+    if capturing:
+        return y  # inside a caller's capture: no host read possible (flags stay on the device)
+    overflow, stale = ovf.tolist()  # one sync: results are never silently clamped or stale
+    if not overflow and not stale:
         return y
-    stats["overflow_reruns"] += 1
+    stats["stale_reruns" if stale else "overflow_reruns"] += 1
     return calibrate(model, x)

@@ -34,10 +34,38 @@ def _req(cond, msg):
         raise ValueError("smpq: " + msg)
 
 
-def quantize_channels_(w2d, bits):
+# Rounding semantics of functions.py:41 `t / scale` (include/smpq.h SMPQ_QSEM_*): torch on the CPU
+# divides (IEEE fp32), torch on the GPU multiplies by fp32(1.0 / scale). "auto" follows the
+# tensor's device, as the reference's own result does; SMPQ_QUANT_SEMANTICS overrides it.
+QSEM = {"cpu": 0, "device": 1}
+_QSEM_MODE = [os.environ.get("SMPQ_QUANT_SEMANTICS", "auto")]
+
+
+def set_quant_semantics(mode):
+    """'auto' (default: device tensors round like torch on the GPU, host tensors like torch on
+    the CPU), 'cpu' or 'device' (every tensor rounds that way)."""
+    if mode not in ("auto", "cpu", "device"):
+        raise ValueError("quant semantics must be 'auto', 'cpu' or 'device'")
+    _QSEM_MODE[0] = mode
+
+
+def get_quant_semantics():
+    return _QSEM_MODE[0]
+
+
+def _qsem(semantics, is_cuda):
+    mode = semantics or _QSEM_MODE[0]
+    if mode == "auto":
+        mode = "device" if is_cuda else "cpu"
+    _req(mode in QSEM, "quant semantics must be 'auto', 'cpu' or 'device'")
+    return QSEM[mode]
+
+
+def quantize_channels_(w2d, bits, semantics=None):
     """In-place fake-quantization of the rows of ``w2d`` (functions.py:25-43 per channel).
 
     w2d: fp32 [cout, k] contiguous (CPU or GPU); bits: int sequence/tensor [cout], 0 = skip.
+    semantics: None (the process setting, ``set_quant_semantics``), 'auto', 'cpu' or 'device'.
     Returns the fp32 step (fp32(scale)) per row (0 for skipped rows) on w2d's device.
     Raises ZeroDivisionError on a constant channel, like the reference (functions.py:40).
     """
@@ -45,6 +73,7 @@ def quantize_channels_(w2d, bits):
          "quantize_channels_: need a contiguous fp32 [cout, k] tensor")
     cout, k = w2d.shape
     lib = _lib.load()
+    sem = _qsem(semantics, w2d.is_cuda)
     bits_t = torch.as_tensor(bits, dtype=torch.int8).reshape(-1)
     _req(bits_t.numel() == cout, "quantize_channels_: bits length != cout")
     _req(bool((bits_t >= 0).all()) and bool((bits_t <= 16).all()), "bits outside [0, 16]")
@@ -53,19 +82,19 @@ def quantize_channels_(w2d, bits):
         step = torch.zeros(cout, dtype=torch.float32, device=w2d.device)
         status = torch.zeros(1, dtype=torch.int32, device=w2d.device)
         with torch.cuda.device(w2d.device):
-            _lib.check(lib.smpq_quantize_channels(_lib.ptr(w2d), cout, k, _lib.ptr(bits_d),
-                                                  _lib.ptr(step), _lib.ptr(status),
-                                                  _lib.stream_ptr()), "smpq_quantize_channels")
+            _lib.check(lib.smpq_quantize_channels_ex(_lib.ptr(w2d), cout, k, _lib.ptr(bits_d),
+                                                     _lib.ptr(step), _lib.ptr(status), sem,
+                                                     _lib.stream_ptr()), "smpq_quantize_channels_ex")
         bad = int(status.item())  # one sync: the reference raises synchronously
         if bad:
             raise ZeroDivisionError("float division by zero (constant channel %d)" % (bad - 1))
         return step
     step = torch.zeros(cout, dtype=torch.float32)
     bits_c = bits_t.contiguous()
-    rc = lib.smpq_quantize_channels_host(_lib.ptr(w2d), cout, k, _lib.ptr(bits_c), _lib.ptr(step))
+    rc = lib.smpq_quantize_channels_host_ex(_lib.ptr(w2d), cout, k, _lib.ptr(bits_c), _lib.ptr(step), sem)
     if rc == _lib.SMPQ_E_CONSTANT:
         raise ZeroDivisionError(_lib.last_error())
-    _lib.check(rc, "smpq_quantize_channels_host")
+    _lib.check(rc, "smpq_quantize_channels_host_ex")
     return step
 
 

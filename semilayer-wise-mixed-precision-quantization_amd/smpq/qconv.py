@@ -54,6 +54,9 @@ class QConv2d(nn.Conv2d):
         self.register_buffer("qstep", torch.zeros(self.out_channels, dtype=torch.float32))
         self._bits_host = np.zeros(self.out_channels, dtype=np.int16)
         self._meta_gen = 0
+        # bumped (smpq.engine) when this conv's caches may hold weight / BN content the host keys
+        # cannot see (a write through `.data` leaves `_version` unchanged)
+        self._content_gen = 0
         self._pack = None
         self.last_path = None
         _REGISTRY.add(self)
@@ -109,8 +112,8 @@ class QConv2d(nn.Conv2d):
     # ---- packing ---------------------------------------------------------------------------
     def _pack_key(self):
         w = self.weight
-        return (w.data_ptr(), w._version, w.device, self._meta_gen, self.qstep.data_ptr(),
-                self.qstep._version, self.qbits._version, ops.get_act_limbs())
+        return (id(w), w.data_ptr(), w._version, w.device, self._meta_gen, id(self.qstep), self.qstep.data_ptr(),
+                self.qstep._version, self.qbits._version, ops.get_act_limbs(), self._content_gen)
 
     def hip_supported(self):
         return (self.weight.is_cuda and self.groups == 1 and self.dilation == (1, 1)

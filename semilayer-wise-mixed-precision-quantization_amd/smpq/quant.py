@@ -2,7 +2,9 @@
 
 ``quantize_wgt`` / ``channel_wise_quantizationperchan`` keep the reference's signatures and
 bit-exact results (host C++ for CPU tensors, a HIP kernel for GPU tensors — both in
-libsmpq.so), and additionally record the (bit, step) metadata on the owning QConv2d.
+libsmpq.so), and additionally record the (bit, step) metadata on the owning QConv2d. The rounding
+of functions.py:41 follows where the tensor lives, as the reference's own result does (torch
+divides on the CPU and multiplies by a reciprocal on the GPU; ops.set_quant_semantics).
 """
 import torch
 
@@ -34,7 +36,7 @@ def channel_wise_quantizationperchan(tensor, bit, i):
     return tensor
 
 
-def quantize_layer_(conv, bits_host):
+def quantize_layer_(conv, bits_host, semantics=None):
     """Vectorised channel_wise_quantizationperchan over a whole conv: one kernel launch.
 
     ``bits_host``: int array [cout], 0 = leave the channel. Per channel the result is
@@ -43,6 +45,6 @@ def quantize_layer_(conv, bits_host):
     w = conv.weight.data
     w2d = w.reshape(w.shape[0], -1)
     assert w2d.data_ptr() == w.data_ptr() and w.is_contiguous()
-    step = ops.quantize_channels_(w2d, bits_host)
+    step = ops.quantize_channels_(w2d, bits_host, semantics=semantics)
     conv.record_quant_all(bits_host, step)
     return step

@@ -84,7 +84,7 @@ def test_reference_pth_runs_exact_int8_path(gpu, tmp_path):
     from smpq import assignments, checkpoint, engine
     torch.manual_seed(0)
     net = resnet.resnet50().to(gpu).eval()
-    assignments.apply_assignment(net, "r50_mixed")
+    assignments.apply_assignment(net, "r50_mixed", semantics="cpu")
     p = tmp_path / "r50.pth"
     torch.save(_plain(net.state_dict()), p)
     torch.manual_seed(1)
@@ -121,3 +121,65 @@ def test_sidecar_shape_mismatch_is_loud(built_lib, tmp_path):
     json.dump(side, open(checkpoint.sidecar_path(p), "w"))
     with pytest.raises(ValueError):
         checkpoint.load_checkpoint(resnet.resnet18(), p, strict=False)
+
+
+def test_plain_pth_has_reference_keys_only(built_lib, tmp_path):
+    # save_checkpoint's default .pth is the reference's format: no qbits/qstep keys, so the
+    # reference's / torchvision's load_state_dict(strict=True) accepts it; strict loading here too
+    import resnet
+    from smpq import checkpoint
+    net = _mixed_net(built_lib)
+    p = tmp_path / "plain.pth"
+    checkpoint.save_checkpoint(net, p)
+    sd = torch.load(p, weights_only=True)
+    assert not any(k.endswith((".qbits", ".qstep")) for k in sd)
+    assert set(sd) == set(_plain(net.state_dict()))
+    net2 = resnet.resnet18()
+    checkpoint.load_checkpoint(net2, p, strict=True)
+    # a key the model does not have is still an error under strict=True
+    sd["bogus.weight"] = torch.zeros(1)
+    torch.save(sd, p)
+    with pytest.raises(RuntimeError):
+        checkpoint.load_checkpoint(resnet.resnet18(), p, strict=True)
+
+
+def test_sidecar_v2_restores_steps_bitwise(built_lib, tmp_path):
+    import resnet
+    from smpq import checkpoint
+    from smpq.assignments import addressable_convs
+    net = _mixed_net(built_lib)
+    p = tmp_path / "v2.pth"
+    checkpoint.save_checkpoint(net, p)
+    steps = checkpoint.read_sidecar_steps(p)
+    for ln, conv in enumerate(addressable_convs(net), start=1):
+        assert np.array_equal(steps[ln].view(np.uint32), conv.qstep.numpy().view(np.uint32)), ln
+    net2 = resnet.resnet18()
+    checkpoint.load_checkpoint(net2, p)
+    for a, b in zip(addressable_convs(net), addressable_convs(net2)):
+        assert torch.equal(a.qbits, b.qbits)
+        assert torch.equal(a.qstep.view(torch.int32), b.qstep.view(torch.int32))
+        assert (a._bits_host == b._bits_host).all()
+
+
+@pytest.mark.gpu
+def test_sidecar_v2_logits_bitwise(gpu, tmp_path):
+    """With the exact steps from the sidecar, a reloaded R50 mixed model's logits equal the
+    original's bit for bit (no ulp-shifted recovered steps)."""
+    import resnet
+    from smpq import assignments, checkpoint, engine
+    torch.manual_seed(0)
+    net = resnet.resnet50().to(gpu).eval()
+    assignments.apply_assignment(net, "r50_mixed", semantics="cpu")
+    p = tmp_path / "r50v2.pth"
+    checkpoint.save_checkpoint(net, p)
+    torch.manual_seed(1)
+    net2 = resnet.resnet50().to(gpu).eval()
+    checkpoint.load_checkpoint(net2, p, map_location=gpu)
+    x = torch.randn(4, 3, 224, 224, generator=torch.Generator().manual_seed(3)).to(gpu)
+    engine.set_range_mode("dynamic")
+    try:
+        with torch.no_grad():
+            a, b = net(x), net2(x)
+    finally:
+        engine.set_range_mode("static")
+    assert torch.equal(a, b)

@@ -10,6 +10,7 @@ Model-level parity: logits of the fused HIP forward vs the reference's CPU logit
 from the reference itself), top-1 identical; tolerance per activation width.
 """
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -36,15 +37,38 @@ def test_mfma_i8_fragment_mapping(gpu):
 
 
 def test_device_quantizer_bitexact_vs_reference(gpu):
+    # CPU semantics on the device: the reference's CPU goldens
     from smpq import ops
     from test_oracle_golden import kat_cases
     for kind, chain, x, y in kat_cases():
         w = torch.from_numpy(x.copy()).reshape(1, -1).to(gpu)
         for b in chain:
-            ops.quantize_channels_(w, [b])
+            ops.quantize_channels_(w, [b], semantics="cpu")
         assert np.array_equal(w.cpu().numpy().ravel().view(np.uint32), y.view(np.uint32)), (kind, chain)
     with pytest.raises(ZeroDivisionError):
         ops.quantize_channels_(torch.full((1, 9), 0.25, device=gpu), [8])
+
+
+def test_device_quantizer_matches_torch_on_gpu(gpu):
+    # default semantics on a device tensor = what torch itself computes for functions.py:41 on the
+    # GPU: the committed device KAT, and torch run live on this box over fresh random channels
+    from smpq import ops
+    import functions
+    from test_oracle_golden import device_kat_cases
+    for kind, chain, x, y in device_kat_cases():
+        w = torch.from_numpy(x.copy()).reshape(1, -1).to(gpu)
+        for b in chain:
+            ops.quantize_channels_(w, [b])
+        assert np.array_equal(w.cpu().numpy().ravel().view(np.uint32), y.view(np.uint32)), (kind, chain)
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_device_kat import quantize_wgt_torch
+    g = torch.Generator().manual_seed(77)
+    for i in range(200):
+        t = (torch.randn((9, 64, 576, 1152)[i % 4], generator=g) * 0.05).to(gpu)
+        b = (8, 6, 4, 2)[(i // 4) % 4]
+        exp = quantize_wgt_torch(t, b)
+        got = functions.quantize_wgt(t, b)
+        assert torch.equal(got.view(torch.int32), exp.view(torch.int32)), (i, b)
 
 
 def test_device_quantizer_layer_matches_host(gpu):
@@ -52,12 +76,13 @@ def test_device_quantizer_layer_matches_host(gpu):
     g = torch.Generator().manual_seed(5)
     w = torch.randn(300, 576, generator=g) * 0.05
     bits = torch.randint(0, 5, (300,), generator=g) * 2  # 0 (skip), 2, 4, 6, 8
-    wd = w.clone().to(gpu)
-    sd = ops.quantize_channels_(wd, bits)
-    wh = w.clone()
-    sh = ops.quantize_channels_(wh, bits)
-    assert torch.equal(wd.cpu().view(torch.int32), wh.view(torch.int32))
-    assert torch.equal(sd.cpu(), sh)
+    for sem in ("cpu", "device"):
+        wd = w.clone().to(gpu)
+        sd = ops.quantize_channels_(wd, bits, semantics=sem)
+        wh = w.clone()
+        sh = ops.quantize_channels_(wh, bits, semantics=sem)
+        assert torch.equal(wd.cpu().view(torch.int32), wh.view(torch.int32)), sem
+        assert torch.equal(sd.cpu(), sh), sem
 
 
 @pytest.mark.parametrize("limbs", [1, 2, 3])
@@ -310,7 +335,8 @@ def build_model(gpu, arch, assign, cal_case=None):
                 sd[k[len(pref):]].copy_(torch.from_numpy(g[k]))
     net = net.to(gpu).eval()
     if assign:
-        assignments.apply_assignment(net, assign)
+        # the goldens are the reference run on the CPU: quantize with torch-CPU rounding
+        assignments.apply_assignment(net, assign, semantics="cpu")
     return net
 
 
@@ -425,8 +451,9 @@ def test_module_path_matches_fused(gpu):
     assert rel < 1.5e-2
 
 
-def test_evaluate_acc_loss_softmax(gpu):
+def test_evaluate_acc_loss_softmax(gpu, monkeypatch):
     import functions
+    monkeypatch.setenv("SMPQ_SYNTHETIC", "1")  # the synthetic loader is opt-in only
     import imagenet
     net = build_model(gpu, "resnet18", "r18_u8")
     loader = imagenet.SyntheticImageNet(n_images=8, batch_size=4)
@@ -776,3 +803,110 @@ def test_forward_independent_of_previous_input(gpu):
                 assert torch.equal(net(x), e1)
     finally:
         engine.USE_GRAPH[0] = use
+
+
+def _fresh_dynamic_logits(gpu, net, x):
+    """Logits of a freshly built model holding net's current state (dynamic ranges, no caches)."""
+    import resnet
+    from smpq import checkpoint, engine
+    fresh = getattr(resnet, "resnet50")().to(gpu).eval()
+    fresh.load_state_dict(net.state_dict())
+    for a, b in zip(net.modules(), fresh.modules()):
+        if hasattr(a, "_bits_host"):
+            b._bits_host = a._bits_host.copy()
+            b._meta_gen += 1
+    prev = engine.get_range_mode()
+    engine.set_range_mode("dynamic")
+    try:
+        with torch.no_grad():
+            return fresh(x)
+    finally:
+        engine.set_range_mode(prev)
+
+
+@pytest.mark.parametrize("mode", ["static", "dynamic"])
+def test_cache_sees_every_kind_of_weight_change(gpu, mode):
+    """the cached forward (packed codes, folded BN, ranges, HIP graph) must never return
+    stale logits — not after a replaced Parameter, load_state_dict(assign=True), a swapped
+    submodule, or writes through .data that leave _version unchanged (caught by the device
+    fingerprint)."""
+    import functions
+    from smpq import engine, stats
+    from smpq.qconv import QConv2d
+    net = build_model(gpu, "resnet50", "r50_mixed")
+    x = torch.randn(4, 3, 224, 224, generator=torch.Generator().manual_seed(31)).to(gpu)
+    engine.set_range_mode(mode)
+    engine.USE_GRAPH[0] = True
+    tol = 2e-4 if mode == "static" else 0.0
+
+    def fwd():
+        with torch.no_grad():
+            net(x)
+            return net(x)  # static: capture / replay path after a change
+
+    def check(tag):
+        y = fwd()
+        ref = _fresh_dynamic_logits(gpu, net, x)
+        err = ((y - ref).abs().max() / ref.abs().max()).item()
+        assert err <= tol, (tag, err)
+        return y
+
+    try:
+        y_prev = check("start")
+        conv = net.layer1[1].conv2
+        # 1. raw .data write of one channel, bypassing the drop-in quantizer (no _version bump)
+        r0 = stats["stale_reruns"]
+        w = conv.weight.data
+        w[5] = functions.quantize_wgt(w[5].clone(), 4)
+        y = check("data-write")
+        assert stats["stale_reruns"] > r0 and not torch.equal(y, y_prev)
+        y_prev = y
+        # 2. .data.copy_ of a whole weight
+        conv3 = net.layer3[2].conv3
+        conv3.weight.data.copy_(conv3.weight.data * 0.5)
+        y = check("data-copy")
+        assert not torch.equal(y, y_prev)
+        y_prev = y
+        # 3. BN buffer through .data
+        net.layer2[0].bn2.running_var.data.mul_(4.0)
+        y = check("bn-data")
+        assert not torch.equal(y, y_prev)
+        y_prev = y
+        # 4. a replaced Parameter (new tensor object)
+        c = net.layer4[0].conv1
+        c.weight = torch.nn.Parameter(c.weight.detach().clone() * 1.5)
+        y = check("param-replace")
+        assert not torch.equal(y, y_prev)
+        y_prev = y
+        # 5. load_state_dict(assign=True)
+        sd = {k: v.clone() for k, v in net.state_dict().items()}
+        sd["layer2.1.conv1.weight"] = sd["layer2.1.conv1.weight"] * 0.75
+        net.load_state_dict(sd, assign=True)
+        y = check("assign")
+        assert not torch.equal(y, y_prev)
+        y_prev = y
+        # 6. a swapped submodule
+        old = net.layer3[1].conv2
+        new = QConv2d(old.in_channels, old.out_channels, 3, padding=1, bias=False).to(gpu)
+        with torch.no_grad():
+            new.weight.copy_(old.weight * -1.0)
+        net.layer3[1].conv2 = new
+        y = check("swap")
+        assert not torch.equal(y, y_prev)
+    finally:
+        engine.set_range_mode("static")
+
+
+def test_device_fingerprint_matches_host(gpu):
+    from smpq.fingerprint import Fingerprinter, host_fingerprint
+    g = torch.Generator().manual_seed(9)
+    ts = [torch.randn(n, generator=g) for n in (16, 70000, 16384, 5)] + [torch.randint(-128, 127, (64,), dtype=torch.int8)]
+    fp = Fingerprinter([t.to(gpu) for t in ts], gpu)
+    got = fp.ref.cpu().numpy().view(np.uint64).tolist()
+    assert got == [host_fingerprint(t) for t in ts]
+    flag = torch.zeros(1, dtype=torch.int32, device=gpu)
+    fp.check(flag)
+    assert int(flag.item()) == 0
+    fp.tensors[1][12345] += 1.0
+    fp.check(flag)
+    assert int(flag.item()) == 1

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from conftest import GOLDEN, REPO
-from test_oracle_golden import kat_cases
+from test_oracle_golden import device_kat_cases, kat_cases
 
 
 def header_symbols():
@@ -33,6 +33,30 @@ def test_host_quantizer_bitexact_vs_reference(built_lib):
         for b in chain:
             ops.quantize_channels_(w, [b])
         assert np.array_equal(w.numpy().ravel().view(np.uint32), y.view(np.uint32)), (kind, chain)
+
+
+def test_host_quantizer_device_semantics_vs_torch_gpu(built_lib):
+    # the host twin with SMPQ_QSEM_DEVICE reproduces what torch computes on the GPU
+    from smpq import ops
+    for kind, chain, x, y in device_kat_cases():
+        w = torch.from_numpy(x.copy()).reshape(1, -1)
+        for b in chain:
+            ops.quantize_channels_(w, [b], semantics="device")
+        assert np.array_equal(w.numpy().ravel().view(np.uint32), y.view(np.uint32)), (kind, chain)
+
+
+def test_quant_semantics_setting(built_lib):
+    from smpq import ops
+    assert ops._qsem(None, False) == 0 and ops._qsem(None, True) == 1  # auto follows the device
+    try:
+        ops.set_quant_semantics("cpu")
+        assert ops._qsem(None, True) == 0
+        ops.set_quant_semantics("device")
+        assert ops._qsem(None, False) == 1
+    finally:
+        ops.set_quant_semantics("auto")
+    with pytest.raises(ValueError):
+        ops.set_quant_semantics("fast")
 
 
 def test_host_quantizer_constant_channel(built_lib):
@@ -106,3 +130,33 @@ def test_dropin_grouping_matches_reference_golden():
     orders = [[int(o[0]), float(o[1])] for o in z["orders"]]
     got = functions.make_quantizedlists(sem, orders)
     np.testing.assert_array_equal(np.array(got, dtype=np.int64), z["quantizedlist"])
+
+
+def test_imagenet_synthetic_is_opt_in(monkeypatch):
+    # a missing dataset raises like the reference (imagenet.py:11-40); synthetic only on SMPQ_SYNTHETIC=1
+    import importlib
+    import sys
+    sys.modules.pop("imagenet", None)
+    monkeypatch.delenv("SMPQ_SYNTHETIC", raising=False)
+    monkeypatch.setenv("SMPQ_IMAGENET_ROOT", "/nonexistent-imagenet")
+    with pytest.raises(Exception):
+        importlib.import_module("imagenet")
+    sys.modules.pop("imagenet", None)
+    monkeypatch.setenv("SMPQ_SYNTHETIC", "1")
+    monkeypatch.setenv("SMPQ_SYNTH_IMAGES", "6")
+    mod = importlib.import_module("imagenet")
+    batches = list(mod.val_loader)
+    assert [b[0].shape[0] for b in batches] == [6] and batches[0][0].shape[1:] == (3, 224, 224)
+    sys.modules.pop("imagenet", None)
+
+
+def test_host_fingerprint_formula(built_lib):
+    # smpq_fingerprint_host = sum_i w_i * (2i + 1) mod 2^64 (the device kernel's formula)
+    from smpq.fingerprint import host_fingerprint
+    t = torch.randn(1000, generator=torch.Generator().manual_seed(3))
+    w = t.numpy().view(np.uint32).astype(np.uint64)
+    exp = int((w * (2 * np.arange(1000, dtype=np.uint64) + 1)).sum(dtype=np.uint64))
+    assert host_fingerprint(t) == exp
+    t2 = t.clone()
+    t2[999] = torch.nextafter(t2[999], torch.tensor(1e9))
+    assert host_fingerprint(t2) != exp
