@@ -258,11 +258,11 @@ int smpq_kl_rows(const float* p_ref, const float* p, int rows, int cols, double*
                  smpq_stream_t stream);
 
 /* ---- content fingerprints (cache validation; smpq/engine.py) ------------------------------------
- * smpq_fingerprint: out[t] = sum_i w_i * (2i + 1) mod 2^64 over the nwords[t] 32-bit words of
+ * smpq_fingerprint: out[t] = sum_i ((w_i * (2i + 1)) mod 2^32) mod 2^64 over the nwords[t] 32-bit words of
  *   tensor t (device pointers ptrs[t], a device array), for t < ntensors; the work is split into
  *   nchunks chunks of smpq_fingerprint_chunk_words() words: chunk c covers tensor chunk_tensor[c]
  *   from word chunk_word[c] (device arrays). out (device uint64 [ntensors]) is overwritten.
- *   Any single-word change changes the fingerprint (odd multipliers are invertible mod 2^64).
+ *   Any single-word change changes the fingerprint (odd multipliers are invertible mod 2^32).
  * smpq_fingerprint_compare: *flag |= 1 if a[i] != b[i] for some i < n (device arrays).
  * smpq_fingerprint_host: the same sum over host memory.
  * Used to detect in-place writes through `.data` (functions.py:22, resnet50_main.py:191) that

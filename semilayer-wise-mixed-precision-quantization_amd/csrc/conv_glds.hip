@@ -40,17 +40,25 @@ constexpr int kAblate = SMPQ_DIAG_ABLATE;
 constexpr unsigned kOOB = 0x80000000u;  // a buffer offset past every range we build (< 2^31 B)
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
-// 16-B store with the default (temporal) or the non-temporal cache policy (gfx950 CPol nt), as
-// inline asm that ends with two wait states (the gfx940-family count): a VMEM store of more than 8 bytes must not have its data
-// VGPRs overwritten by the very next instruction, and ROCm 7.2's gfx950 hazard recognizer does not
-// always separate them (observed: dword 0 of a limb-plane store intermittently replaced by the
-// register's next value when a v_mov to it directly followed the store). nt is wave-uniform.
+// Inline-asm VMEM instructions are invisible to the compiler's hazard recognizer, so they carry
+// their own wait states on both sides:
+//  * before: 5 (s_nop 4) — a VALU write of an SGPR (v_readfirstlane / v_readlane, e.g. an SGPR
+//    restored from a VGPR lane under SGPR pressure) needs 5 wait states before a VMEM instruction
+//    reads it as soffset / resource (observed: a limb-plane store whose soffset came from a
+//    v_readlane one instruction earlier wrote its plane at a stale offset);
+//  * after (stores): 2 (s_nop 1) — a VMEM store of more than 8 bytes must not have its data VGPRs
+//    overwritten by the very next instruction (observed: dword 0 of a limb-plane store replaced by
+//    the register's next value when a v_mov to it directly followed the store).
+// 16-B store with the default (temporal) or the non-temporal cache policy (gfx950 CPol nt); nt is
+// wave-uniform.
 __device__ __forceinline__ void store_limbs16(v4u v, v4i rs, unsigned off, unsigned soff, bool nt) {
   if (nt)
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen nt\n\ts_nop 1" ::"v"(v), "v"(off), "s"(rs), "s"(soff)
+    asm volatile("s_nop 4\n\tbuffer_store_dwordx4 %0, %1, %2, %3 offen nt\n\ts_nop 1" ::"v"(v), "v"(off), "s"(rs),
+                 "s"(soff)
                  : "memory");
   else
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(off), "s"(rs), "s"(soff)
+    asm volatile("s_nop 4\n\tbuffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(off), "s"(rs),
+                 "s"(soff)
                  : "memory");
 }
 
@@ -67,10 +75,13 @@ __device__ __forceinline__ v4i make_rsrc(const void* base, long long bytes) {
   return r;
 }
 
-// One 1-KiB piece: lane i's 16 bytes at rsrc[voff + soff] -> LDS [lds + 16 i, +16).
+// One 1-KiB piece: lane i's 16 bytes at rsrc[voff + soff] -> LDS [lds + 16 i, +16). The leading
+// s_nop 1, the two s_movs and the s_nop 0 give the 5 wait states a VALU-written soffset / resource SGPR needs
+// (see store_limbs16); the s_nop 0 separates the M0 write from the LDS DMA.
 __device__ __forceinline__ void dma16(unsigned lds, v4i rsrc, unsigned voff, unsigned soff) {
   unsigned keep;
   asm volatile(
+      "s_nop 1\n\t"
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
@@ -162,7 +173,12 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // NST LDS stages: the DMA of K step k + NST - 1 is in flight while step k computes.
 // BK: K bytes per stage and row. 64 = one MFMA K; 128 (cin % 128 == 0) = two, and every DMA piece
 // is then 8 whole 128-B lines instead of 16 half lines (half the TA/TD work per byte).
-template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK>
+// LEAN: the static-range epilogue that only emits the next conv's limb planes (no fp32 output, no
+// fp32 residual, no per-image maxima): the output quantizer's 1/step is folded into the column
+// scale / shift and the residual scale, ReLU and the code clamp are one v_med3, and overflow is
+// tracked on the rounded codes — about half the VALU work of the general epilogue per output.
+template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
+          bool LEAN = false>
 __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kernel(ConvArgs a) {
   static_assert(BK == 64 || BK == 128, "BK");
   static_assert(!S2D || BK == 64, "the s2d stem uses 64-B K steps");
@@ -578,98 +594,172 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 #pragma unroll
       for (int j = 0; j < WP; ++j) decode4<L>(rw[i][j], rqv[i][j]);
   }
-  // limb recombination + affine + residual, two channels at a time (v_pk_* fp32 ops round like
-  // their scalar forms: the same bits as conv.hip's epilogue)
-  float o[WC][WP][4];
-#pragma unroll
-  for (int i = 0; i < WC; ++i) {
-    const int c = chan[i] < a.cout ? chan[i] : 0;
-    const float4 cs = *reinterpret_cast<const float4*>(a.col_scale + c);
-    const float4 csh = *reinterpret_cast<const float4*>(a.col_shift + c);
-    const f2 csr[2] = {f2{cs.x, cs.y}, f2{cs.z, cs.w}};
-    const f2 shr[2] = {f2{csh.x, csh.y}, f2{csh.z, csh.w}};
-#pragma unroll
-    for (int j = 0; j < WP; ++j) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        f2 v;
-#pragma unroll
-        for (int s = 0; s < NACC; ++s) {
-          const int t0 = acc[s][i][j][2 * h], t1 = acc[s][i][j][2 * h + 1];
-          const f2 tf = f2{(float)t0, (float)t1};
-          constexpr float w0 = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
-          const float lw = w0 * (float)(1 << (8 * s));
-          // fma(x, 1, 0) == x for x = (float)int (never -0): the first limb is a plain convert
-          v = s == 0 ? (SMIN == 0 ? tf : tf * f2{lw, lw}) : __builtin_elementwise_fma(tf, f2{lw, lw}, v);
-        }
-        const f2 sc = f2{rscale[j], rscale[j]} * csr[h];
-        f2 out = __builtin_elementwise_fma(v, sc, shr[h]);
-        if (a.res_q)
-          out = out + f2{a.res_scale, a.res_scale} * f2{(float)rqv[i][j][2 * h], (float)rqv[i][j][2 * h + 1]};
-        o[i][j][2 * h] = out.x;
-        o[i][j][2 * h + 1] = out.y;
-      }
-    }
-  }
-  if (a.residual && !a.res_q) {
-    const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.residual), 0, (int)(4 * oplane),
-                                                       0x00020000);
-    v4u rv[WC][WP];
-#pragma unroll
-    for (int i = 0; i < WC; ++i)
-#pragma unroll
-      for (int j = 0; j < WP; ++j) rv[i][j] = __builtin_amdgcn_raw_buffer_load_b128(rrs, f32_off(ooff[i][j]), 0, 0);
-#pragma unroll
-    for (int i = 0; i < WC; ++i)
-#pragma unroll
-      for (int j = 0; j < WP; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[i][j][r] = __fadd_rn(o[i][j][r], __uint_as_float(rv[i][j][r]));
-  }
-  if (a.relu) {
-#pragma unroll
-    for (int i = 0; i < WC; ++i)
-#pragma unroll
-      for (int j = 0; j < WP; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[i][j][r] = fmaxf(o[i][j][r], 0.f);
-  }
-  if (a.y) {
-    const v4i yrs4 = make_rsrc(a.y, 4LL * oplane);
-#pragma unroll
-    for (int i = 0; i < WC; ++i)
-#pragma unroll
-      for (int j = 0; j < WP; ++j) {
-        const v4u v = {__float_as_uint(o[i][j][0]), __float_as_uint(o[i][j][1]), __float_as_uint(o[i][j][2]),
-                       __float_as_uint(o[i][j][3])};
-        store_limbs16(v, yrs4, f32_off(ooff[i][j]), 0u, false);
-      }
-  }
   constexpr float qmax = act_qmax<L>();
-  if (a.yq) {
-    // fused quantizer of the next conv's input (static range): one dword per limb plane
-    const auto qrs = __builtin_amdgcn_make_buffer_rsrc(a.yq, 0, (int)(L * oplane), 0x00020000);
-    const v4i qrs4 = make_rsrc(a.yq, (long long)L * oplane);
-    const bool nt = __builtin_amdgcn_readfirstlane(a.nt_store) != 0;
-    float vmax = 0.f;
-    unsigned wq[WC][WP][L];
+  // limb recombination of the accumulators: v = sum_s fl(acc_s) * 256^(SMIN + s), two channels at
+  // a time (v_pk_* fp32 ops round like their scalar forms: the same bits as conv.hip's epilogue)
+  auto combine = [&](int i, int j, int h) {
+    f2 v;
 #pragma unroll
-    for (int i = 0; i < WC; ++i)
+    for (int s = 0; s < NACC; ++s) {
+      const int t0 = acc[s][i][j][2 * h], t1 = acc[s][i][j][2 * h + 1];
+      const f2 tf = f2{(float)t0, (float)t1};
+      constexpr float w0 = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
+      const float lw = w0 * (float)(1 << (8 * s));
+      // fma(x, 1, 0) == x for x = (float)int (never -0): the first limb is a plain convert
+      v = s == 0 ? (SMIN == 0 ? tf : tf * f2{lw, lw}) : __builtin_elementwise_fma(tf, f2{lw, lw}, v);
+    }
+    return v;
+  };
+  unsigned wq[WC][WP][L];
+  float vmax = 0.f;
+  if constexpr (LEAN) {
+    // z = v * (rscale * col_scale / step_out) + col_shift / step_out [+ r * res_scale / step_out];
+    // code = med3(rne(z), relu ? 0 : -QMAX, QMAX). Scalar fp32 ops: the packed forms need
+    // register pairs and cost more moves than they save here.
+    const float inv = a.yq_inv;
+    const float rsq = a.res_scale * inv;
+    const float lo = a.relu ? 0.f : -qmax;
+    const bool has_res = a.res_q != nullptr;
+    const bool relu = a.relu != 0;
+    constexpr float w0 = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
+#pragma unroll
+    for (int i = 0; i < WC; ++i) {
+      const int c = chan[i] < a.cout ? chan[i] : 0;
+      const float4 cs = *reinterpret_cast<const float4*>(a.col_scale + c);
+      const float4 csh = *reinterpret_cast<const float4*>(a.col_shift + c);
+      const float csq[4] = {cs.x * inv, cs.y * inv, cs.z * inv, cs.w * inv};
+      const float shq[4] = {csh.x * inv, csh.y * inv, csh.z * inv, csh.w * inv};
 #pragma unroll
       for (int j = 0; j < WP; ++j) {
         int q[4];
-        float am = 0.f;
+        float m = 0.f;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const f2 z = f2{o[i][j][2 * h], o[i][j][2 * h + 1]} * f2{a.yq_inv, a.yq_inv};
-          q[2 * h] = (int)fminf(fmaxf(rintf(z.x), -qmax), qmax);
-          q[2 * h + 1] = (int)fminf(fmaxf(rintf(z.y), -qmax), qmax);
+        for (int r = 0; r < 4; ++r) {
+          float v = (float)acc[0][i][j][r];
+          if (SMIN != 0) v = v * w0;
+#pragma unroll
+          for (int t = 1; t < NACC; ++t) v = __fmaf_rn((float)acc[t][i][j][r], w0 * (float)(1 << (8 * t)), v);
+          float z = __fmaf_rn(v, rscale[j] * csq[r], shq[r]);
+          if (has_res) z = __fmaf_rn((float)rqv[i][j][r], rsq, z);
+          const float zr = rintf(z);
+          m = fmaxf(m, relu ? zr : fabsf(zr));
+          q[r] = (int)__builtin_amdgcn_fmed3f(zr, lo, qmax);
         }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) am = fmaxf(am, fabsf(o[i][j][r]));
-        vmax = ooff[i][j] != kOOB ? fmaxf(vmax, am) : vmax;
+        vmax = ooff[i][j] != kOOB ? fmaxf(vmax, m) : vmax;
         encode4<L>(q, wq[i][j]);
       }
+    }
+  } else {
+    float o[WC][WP][4];
+#pragma unroll
+    for (int i = 0; i < WC; ++i) {
+      const int c = chan[i] < a.cout ? chan[i] : 0;
+      const float4 cs = *reinterpret_cast<const float4*>(a.col_scale + c);
+      const float4 csh = *reinterpret_cast<const float4*>(a.col_shift + c);
+      const f2 csr[2] = {f2{cs.x, cs.y}, f2{cs.z, cs.w}};
+      const f2 shr[2] = {f2{csh.x, csh.y}, f2{csh.z, csh.w}};
+#pragma unroll
+      for (int j = 0; j < WP; ++j) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f2 sc = f2{rscale[j], rscale[j]} * csr[h];
+          f2 out = __builtin_elementwise_fma(combine(i, j, h), sc, shr[h]);
+          if (a.res_q)
+            out = out + f2{a.res_scale, a.res_scale} * f2{(float)rqv[i][j][2 * h], (float)rqv[i][j][2 * h + 1]};
+          o[i][j][2 * h] = out.x;
+          o[i][j][2 * h + 1] = out.y;
+        }
+      }
+    }
+    if (a.residual && !a.res_q) {
+      const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.residual), 0, (int)(4 * oplane),
+                                                         0x00020000);
+      v4u rv[WC][WP];
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) rv[i][j] = __builtin_amdgcn_raw_buffer_load_b128(rrs, f32_off(ooff[i][j]), 0, 0);
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+#pragma unroll
+        for (int j = 0; j < WP; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[i][j][r] = __fadd_rn(o[i][j][r], __uint_as_float(rv[i][j][r]));
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+#pragma unroll
+        for (int j = 0; j < WP; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[i][j][r] = fmaxf(o[i][j][r], 0.f);
+    }
+    if (a.y) {
+      const v4i yrs4 = make_rsrc(a.y, 4LL * oplane);
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+          const v4u v = {__float_as_uint(o[i][j][0]), __float_as_uint(o[i][j][1]), __float_as_uint(o[i][j][2]),
+                         __float_as_uint(o[i][j][3])};
+          store_limbs16(v, yrs4, f32_off(ooff[i][j]), 0u, false);
+        }
+    }
+    if (a.yq) {
+      // fused quantizer of the next conv's input (static range)
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+          int q[4];
+          float am = 0.f;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const f2 z = f2{o[i][j][2 * h], o[i][j][2 * h + 1]} * f2{a.yq_inv, a.yq_inv};
+            q[2 * h] = (int)fminf(fmaxf(rintf(z.x), -qmax), qmax);
+            q[2 * h + 1] = (int)fminf(fmaxf(rintf(z.y), -qmax), qmax);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) am = fmaxf(am, fabsf(o[i][j][r]));
+          vmax = ooff[i][j] != kOOB ? fmaxf(vmax, am) : vmax;
+          encode4<L>(q, wq[i][j]);
+        }
+    }
+    if (a.y_absmax) {
+      float pmax[WP];  // per pixel max |y| over this lane's channels, then over the 4 lane groups
+#pragma unroll
+      for (int j = 0; j < WP; ++j) {
+        float am = 0.f;
+#pragma unroll
+        for (int i = 0; i < WC; ++i)
+          if (ooff[i][j] != kOOB)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) am = fmaxf(am, fabsf(o[i][j][r]));
+        am = fmaxf(am, __shfl_xor(am, 16, kWave));
+        pmax[j] = fmaxf(am, __shfl_xor(am, 32, kWave));
+      }
+      const int mfirst = m0 + wp * WP * 16;
+      const int mlast = min(mfirst + WP * 16, a.M) - 1;
+      if (mfirst <= mlast) {
+        const int img_lo = fast_div(mfirst, a.hw_mul, a.hw_shr), img_hi = fast_div(mlast, a.hw_mul, a.hw_shr);
+        if (img_lo == img_hi) {
+          float v = 0.f;
+#pragma unroll
+          for (int j = 0; j < WP; ++j) v = fmaxf(v, pmax[j]);
+          v = wave_max(v);
+          if (lane == 0 && v > 0.f) atomic_max_nonneg(&a.y_absmax[img_lo], v);
+        } else if (lane < 16) {
+#pragma unroll
+          for (int j = 0; j < WP; ++j)
+            if (mok[j] && pmax[j] > 0.f) atomic_max_nonneg(&a.y_absmax[fast_div(mrow[j], a.hw_mul, a.hw_shr)], pmax[j]);
+        }
+      }
+    }
+  }
+  if (a.yq) {
+    const auto qrs = __builtin_amdgcn_make_buffer_rsrc(a.yq, 0, (int)(L * oplane), 0x00020000);
+    const v4i qrs4 = make_rsrc(a.yq, (long long)L * oplane);
+    const bool nt = __builtin_amdgcn_readfirstlane(a.nt_store) != 0;
     if (TR && !stage_out) {
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
@@ -719,39 +809,9 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
             if (!(kAblate & 2) || wq[i][j][l] == 0x12345679u)
               __builtin_amdgcn_raw_buffer_store_b32(wq[i][j][l], qrs, ooff[i][j], (unsigned)((long long)l * oplane), 0);
     }
-    // |rne(y * inv)| is monotone in |y|: one test on the lane's max
-    const bool ovf = rintf(__fmul_rn(vmax, a.yq_inv)) > qmax;
+    // LEAN: vmax is the largest rounded code; otherwise max |y| (|rne(y * inv)| is monotone in |y|)
+    const bool ovf = LEAN ? vmax > qmax : rintf(__fmul_rn(vmax, a.yq_inv)) > qmax;
     if (__any(ovf) && lane == 0) atomicMax(a.overflow, 1);
-  }
-  if (a.y_absmax) {
-    float pmax[WP];  // per pixel max |y| over this lane's channels, then over the 4 lane groups
-#pragma unroll
-    for (int j = 0; j < WP; ++j) {
-      float am = 0.f;
-#pragma unroll
-      for (int i = 0; i < WC; ++i)
-        if (ooff[i][j] != kOOB)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) am = fmaxf(am, fabsf(o[i][j][r]));
-      am = fmaxf(am, __shfl_xor(am, 16, kWave));
-      pmax[j] = fmaxf(am, __shfl_xor(am, 32, kWave));
-    }
-    const int mfirst = m0 + wp * WP * 16;
-    const int mlast = min(mfirst + WP * 16, a.M) - 1;
-    if (mfirst <= mlast) {
-      const int img_lo = fast_div(mfirst, a.hw_mul, a.hw_shr), img_hi = fast_div(mlast, a.hw_mul, a.hw_shr);
-      if (img_lo == img_hi) {
-        float v = 0.f;
-#pragma unroll
-        for (int j = 0; j < WP; ++j) v = fmaxf(v, pmax[j]);
-        v = wave_max(v);
-        if (lane == 0 && v > 0.f) atomic_max_nonneg(&a.y_absmax[img_lo], v);
-      } else if (lane < 16) {
-#pragma unroll
-        for (int j = 0; j < WP; ++j)
-          if (mok[j] && pmax[j] > 0.f) atomic_max_nonneg(&a.y_absmax[fast_div(mrow[j], a.hw_mul, a.hw_shr)], pmax[j]);
-      }
-    }
   }
 }
 
@@ -794,6 +854,11 @@ constexpr GldsCfg kGlds[] = {
     {1, 4, 4, 1, 4, 64},   // 24: as 3, 4 stages
     {2, 2, 4, 2, 3, 128},  // 25: as 18, 3 stages
     {2, 2, 2, 2, 3, 128},  // 26: as 16, 3 stages
+    // wide channel tiles: fewer L2->LDS bytes per MAC (the long-K convs are bound by the ~30 B/clk
+    // per CU an LDS fill gets from L2, not by the MFMAs)
+    {4, 2, 4, 2, 2, 128},  // 27: 256 ch x  64 px, 8 waves, 128-B K steps
+    {4, 2, 4, 2, 3, 64},   // 28: 256 ch x  64 px, 8 waves, 3 stages
+    {4, 4, 4, 2, 2, 64},   // 29: 256 ch x 128 px, 16 waves
 };
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
@@ -842,7 +907,6 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
       return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: 128-wide K steps need cin % 128 == 0");
     constexpr int STAGE = (LW * BC + L * BP) * BK;
     constexpr int kMaxLds = 160 * 1024;  // LDS per CU on gfx950
-    auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK>;
     // no more stages than K steps: a single-step conv (1x1, cin 64) needs one
     const int nsteps = a.ksteps / (BK / 64);
     // operand stages, enlarged to hold the staged output tile, + the residual tile (kernel layout)
@@ -854,16 +918,23 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
     if (TRT && lines && a.res_q) lds_bytes += TILEB;
     if (lds_bytes > kMaxLds) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: tile config needs more LDS than a CU has");
     constexpr int kMaxNeed = (NST * STAGE > TILEB ? NST * STAGE : TILEB) + TILEB;
-    static const hipError_t attr = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-        kMaxNeed < kMaxLds ? kMaxNeed : kMaxLds);
-    if (attr != hipSuccess) {
-      (void)hipGetLastError();  // do not leave the error for the next, unrelated launch to report
-      return check_hip(attr, "qconv_glds_kernel LDS attribute");
-    }
     ConvArgs b = a;
     fast_div_init((int)nt, b.ntc_mul, b.ntc_shr);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(mt * nt)), dim3(64 * WAVES_C * WAVES_P), lds_bytes, stream, b);
+    const bool lean = L >= 2 && a.yq && !a.y && !a.residual && !a.y_absmax;
+    auto kfull = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, false>;
+    auto klean = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, (L >= 2)>;
+    auto set_lds = [](const void* k) {
+      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               kMaxNeed < kMaxLds ? kMaxNeed : kMaxLds);
+      if (e != hipSuccess) (void)hipGetLastError();  // do not leave it for an unrelated launch to report
+      return e;
+    };
+    static const hipError_t attr_full = set_lds(reinterpret_cast<const void*>(kfull));
+    static const hipError_t attr_lean = set_lds(reinterpret_cast<const void*>(klean));
+    const hipError_t attr = lean ? attr_lean : attr_full;
+    if (attr != hipSuccess) return check_hip(attr, "qconv_glds_kernel LDS attribute");
+    hipLaunchKernelGGL(lean ? klean : kfull, dim3((unsigned)(mt * nt)), dim3(64 * WAVES_C * WAVES_P), lds_bytes,
+                       stream, b);
     return check_hip(hipGetLastError(), "qconv_glds_kernel launch");
   }
 }
@@ -898,6 +969,9 @@ static int launch_cfg(int cfg, const ConvArgs& a, hipStream_t s) {
     case 24: return launch_one<L, LW, 1, 4, 4, 1, false, 4>(a, s);
     case 25: return launch_one<L, LW, 2, 2, 4, 2, false, 3, 2, 128>(a, s);
     case 26: return launch_one<L, LW, 2, 2, 2, 2, false, 3, 2, 128>(a, s);
+    case 27: return launch_one<L, LW, 4, 2, 4, 2, false, 2, 1, 128>(a, s);
+    case 28: return launch_one<L, LW, 4, 2, 4, 2, false, 3, 1, 64>(a, s);
+    case 29: return launch_one<L, LW, 4, 4, 4, 2, false, 2, 1, 64>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   }
 }

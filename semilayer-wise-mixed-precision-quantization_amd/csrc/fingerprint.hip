@@ -9,8 +9,9 @@
 // caches were built; a mismatch is reported with the overflow flag it already reads once per
 // forward, and the result is recomputed from freshly packed weights.
 //
-// Fingerprint of a tensor of N 32-bit words w_i: sum_i w_i * (2i + 1) mod 2^64. Every odd
-// multiplier is invertible mod 2^64, so any change of a single word changes the sum; the sum is
+// Fingerprint of a tensor of N 32-bit words w_i: sum_i ((w_i * (2i + 1)) mod 2^32) mod 2^64. An
+// odd multiplier is invertible mod 2^32, so changing a single word changes its product and hence
+// the sum (the products are summed as integers, never wrapped below 2^64); the sum is
 // order-independent (exact integer atomics), hence deterministic. Work is split into chunks of
 // kChunkWords words; chunk c belongs to tensor chunk_tensor[c] and starts at word chunk_word[c].
 // HBM-bound: one read of every byte (R50: ~100 MB of fp32 weights, ~15-20 us).
@@ -34,8 +35,22 @@ __global__ __launch_bounds__(kFpThreads) void fingerprint_kernel(const uint32_t*
   const long long w1 = w0 + kChunkWords < n ? w0 + kChunkWords : n;
   const uint32_t* p = ptrs[t];
   unsigned long long acc = 0;
-  for (long long i = w0 + threadIdx.x; i < w1; i += kFpThreads)
-    acc += (unsigned long long)p[i] * (unsigned long long)(2 * i + 1);
+  // 16-B loads where the chunk is whole quads (tensors start 16-B aligned: caching-allocator blocks)
+  const bool vec = ((reinterpret_cast<unsigned long long>(p) & 15) == 0) && ((w1 - w0) & 3) == 0;
+  if (vec) {
+    const uint4* q = reinterpret_cast<const uint4*>(p + w0);
+    const int nq = (int)((w1 - w0) >> 2);
+    const unsigned base = (unsigned)(2 * w0 + 1);
+    for (int j = threadIdx.x; j < nq; j += kFpThreads) {
+      const uint4 v = q[j];
+      const unsigned m = base + 8u * (unsigned)j;  // 2i + 1 for i = w0 + 4j (mod 2^32)
+      acc += (unsigned long long)(v.x * m) + (unsigned long long)(v.y * (m + 2u)) +
+             (unsigned long long)(v.z * (m + 4u)) + (unsigned long long)(v.w * (m + 6u));
+    }
+  } else {
+    for (long long i = w0 + threadIdx.x; i < w1; i += kFpThreads)
+      acc += (unsigned long long)(p[i] * (unsigned)(2 * i + 1));
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, kWave);
   const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
@@ -95,6 +110,6 @@ extern "C" int smpq_fingerprint_compare(const uint64_t* a, const uint64_t* b, in
 extern "C" uint64_t smpq_fingerprint_host(const void* p, int64_t nwords) {
   const uint32_t* w = static_cast<const uint32_t*>(p);
   unsigned long long acc = 0;
-  for (long long i = 0; i < nwords; ++i) acc += (unsigned long long)w[i] * (unsigned long long)(2 * i + 1);
+  for (long long i = 0; i < nwords; ++i) acc += (unsigned long long)(w[i] * (unsigned)(2 * i + 1));
   return acc;
 }

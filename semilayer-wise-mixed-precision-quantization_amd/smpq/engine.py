@@ -41,12 +41,14 @@ from . import ops
 from .fingerprint import Fingerprinter
 from .qconv import QConv2d, stats
 
-_MODE = ["static"]
+import os as _os
+# "dynamic" is the deterministic mode for search runs (each image's logits depend on nothing but
+# the weights and that image); "static" (default) is the fast mode (range modes)
+_MODE = [_os.environ.get("SMPQ_RANGE_MODE", "static")]
 HEADROOM = 2.0
 # images per pass through the network: a chunk's inter-layer activations (int8 limb planes) stay
 # resident in the 256 MiB Infinity Cache between producer and consumer instead of round-tripping
 # HBM; every image is independent, so chunking changes no result (fc runs once on all features)
-import os as _os
 CHUNK = [int(_os.environ.get("SMPQ_CHUNK", "256"))]
 # replay the static-range forward from a captured HIP graph (one launch instead of ~60 kernels
 # with their Python/ctypes host cost); recaptured when weights, BN, ranges or shapes change

@@ -310,6 +310,58 @@ def test_static_outputs_identical_across_tiles(gpu, shape, limbs, range_frac):
     assert int(ovf0.item()) == (1 if range_frac < 1 else 0)
 
 
+@pytest.mark.parametrize("relu", [True, False])
+@pytest.mark.parametrize("range_frac", [2.0, 0.5])
+@pytest.mark.parametrize("limbs", [2, 3])
+@pytest.mark.parametrize("shape", [(64, 256, 1, 1, 20), (128, 64, 3, 2, 17), (64, 80, 3, 1, 9), (256, 128, 1, 1, 12)],
+                         ids=lambda s: "c%d_o%d_k%d_s%d_h%d" % s)
+def test_lean_static_epilogue(gpu, shape, limbs, range_frac, relu):
+    """The lean static epilogue (limb planes only: the engine's block-internal convs) folds 1/step
+    into the column scale: its codes agree bitwise across every tile config, are within one code
+    of clamp(rne(y * QMAX / range)) of the general epilogue's fp32 y (and equal almost always),
+    and it raises the overflow flag exactly when the general epilogue does."""
+    from smpq import ops
+    cin, cout, k, s, h = shape
+    wd, step, codes, offset = make_layer(gpu, cin, cout, k, seed=cin + 7 * cout)
+    g = torch.Generator().manual_seed(12)
+    x = torch.relu(torch.randn(3, h, h, cin, generator=g)).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, limbs)
+    ho = (h + 2 * (k // 2) - k) // s + 1
+    rq = ops.act_quantize(torch.randn(3, ho, ho, cout, generator=g).clamp(-4, 4).to(gpu),
+                          torch.full((3,), 4.0, device=gpu), limbs)
+    shift = torch.linspace(-1, 1, cout, device=gpu)
+    kw = dict(relu=relu, residual_q=rq, residual_range=4.0)
+    ref = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, **kw)
+    rng = float(ref.abs().max()) * range_frac
+    outs = []
+    for c in ops.tile_configs():
+        if not ops._tile_fits(c, limbs, 1, False, cout, cin, k) or ops.tile_kind(c) not in (ops.TILE_LDS_DMA,
+                                                                                            ops.TILE_LDS_DMA_K128):
+            continue
+        ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+        y, yq = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, tile_cfg=c,
+                             emit_range=rng, overflow=ovf, want_f32=False, **kw)
+        assert y is None
+        outs.append((c, yq, ovf))
+    c0, yq0, ovf0 = outs[0]
+    for c, yq, ovf in outs[1:]:
+        assert torch.equal(yq, yq0), c
+        assert torch.equal(ovf, ovf0), c
+    ovf_full = torch.zeros(1, dtype=torch.int32, device=gpu)
+    yf, yqf = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, tile_cfg=outs[0][0],
+                           emit_range=rng, overflow=ovf_full, want_f32=True, **kw)
+    assert torch.equal(yf, ref)
+    lean = sum(yq0[l].cpu().numpy().astype(np.int64) * 256 ** l for l in range(limbs))
+    full = sum(yqf[l].cpu().numpy().astype(np.int64) * 256 ** l for l in range(limbs))
+    # at 24 bits a code unit is about one fp32 ulp of z: the two formulas' roundings differ there
+    diff = np.abs(lean - full)
+    assert diff.max() <= (1 if limbs == 2 else 2) and (diff != 0).mean() < (0.01 if limbs == 2 else 0.05)
+    if relu:
+        assert lean.min() >= 0
+    assert int(ovf0.item()) == int(ovf_full.item()) == (1 if range_frac < 1 else 0)
+
+
 def test_conv_offsets_exercised(gpu):
     # 8-bit channels need a code offset whenever their code range is not inside [-128, 127]
     off = run_conv_case(gpu, 256, 256, 1, 1, 14, limbs=2, seed=3)

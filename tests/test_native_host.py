@@ -151,11 +151,12 @@ def test_imagenet_synthetic_is_opt_in(monkeypatch):
 
 
 def test_host_fingerprint_formula(built_lib):
-    # smpq_fingerprint_host = sum_i w_i * (2i + 1) mod 2^64 (the device kernel's formula)
+    # smpq_fingerprint_host = sum_i ((w_i * (2i + 1)) mod 2^32) mod 2^64 (the device kernel's formula)
     from smpq.fingerprint import host_fingerprint
     t = torch.randn(1000, generator=torch.Generator().manual_seed(3))
     w = t.numpy().view(np.uint32).astype(np.uint64)
-    exp = int((w * (2 * np.arange(1000, dtype=np.uint64) + 1)).sum(dtype=np.uint64))
+    prod = (w * (2 * np.arange(1000, dtype=np.uint64) + 1)) % (1 << 32)
+    exp = int(prod.sum(dtype=np.uint64))
     assert host_fingerprint(t) == exp
     t2 = t.clone()
     t2[999] = torch.nextafter(t2[999], torch.tensor(1e9))
