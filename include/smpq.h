@@ -214,6 +214,19 @@ int smpq_stem_conv_s2d_q(const int8_t* xq, const float* x_absmax, int n, int h, 
                          int limbs, float* y, float* y_absmax, int8_t* yq, float yq_range, int32_t* overflow,
                          int tile_cfg, smpq_stream_t stream);
 
+/* Fused stem, static-range mode: conv1 7x7/2/3 + bn1 + ReLU + maxpool 3x3/2/1 (resnet.py:143-147,
+ * ResNet.forward resnet.py:206-209) in one launch, on smpq_image_quantize_s2d planes and
+ * smpq_pack_weights_s2d codes -> the POOLED output's limb planes yq [limbs][n][h/4][w/4][64]
+ * (h, w = the original image size). Bitwise identical to smpq_stem_conv_s2d_q (relu = 1, yq with
+ * the same range, y = NULL) followed by smpq_maxpool_limbs; *overflow is set to 1 when a conv
+ * output exceeded the range (then clamped). smpq_stem_pool_supported returns 1 for the shapes it
+ * handles: cout == 64, h and w multiples of 4, w <= 224, (limbs, wlimbs) in {(3,3), (2,2), (1,2)};
+ * otherwise use the two-launch path. */
+int smpq_stem_pool_supported(int n, int h, int w, int cout, int limbs, int wlimbs);
+int smpq_stem_pool_s2d_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, const int8_t* codes,
+                         int wlimbs, int cout, const float* col_scale, const float* col_shift, int limbs,
+                         int8_t* yq, float yq_range, int32_t* overflow, smpq_stream_t stream);
+
 /* Tile configurations of smpq_conv2d_fwd (for autotuning): count, and BM (pixels) x BN (output
  * channels) / threads. Every configuration gives bitwise-identical results. */
 int smpq_conv2d_num_tile_configs(void);
@@ -258,11 +271,13 @@ int smpq_kl_rows(const float* p_ref, const float* p, int rows, int cols, double*
                  smpq_stream_t stream);
 
 /* ---- content fingerprints (cache validation; smpq/engine.py) ------------------------------------
- * smpq_fingerprint: out[t] = sum_i ((w_i * (2i + 1)) mod 2^32) mod 2^64 over the nwords[t] 32-bit words of
+ * smpq_fingerprint: out[t] = sum_i H(w_i, i) mod 2^64 over the nwords[t] 32-bit words of
  *   tensor t (device pointers ptrs[t], a device array), for t < ntensors; the work is split into
  *   nchunks chunks of smpq_fingerprint_chunk_words() words: chunk c covers tensor chunk_tensor[c]
  *   from word chunk_word[c] (device arrays). out (device uint64 [ntensors]) is overwritten.
- *   Any single-word change changes the fingerprint (odd multipliers are invertible mod 2^32).
+ *   H(w, i) = fmix32(w ^ i*0x9E3779B9) | fmix32(w ^ (i*0x85EBCA6B + 0xC2B2AE35)) << 32, fmix32 = the
+ *   MurmurHash3 finalizer (all arithmetic mod 2^32): injective in w for each i, so any single-word
+ *   change changes the fingerprint, and structured multi-word changes cancel with p ~ 2^-64.
  * smpq_fingerprint_compare: *flag |= 1 if a[i] != b[i] for some i < n (device arrays).
  * smpq_fingerprint_host: the same sum over host memory.
  * Used to detect in-place writes through `.data` (functions.py:22, resnet50_main.py:191) that

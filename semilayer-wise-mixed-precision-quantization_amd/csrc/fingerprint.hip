@@ -9,17 +9,35 @@
 // caches were built; a mismatch is reported with the overflow flag it already reads once per
 // forward, and the result is recomputed from freshly packed weights.
 //
-// Fingerprint of a tensor of N 32-bit words w_i: sum_i ((w_i * (2i + 1)) mod 2^32) mod 2^64. An
-// odd multiplier is invertible mod 2^32, so changing a single word changes its product and hence
-// the sum (the products are summed as integers, never wrapped below 2^64); the sum is
-// order-independent (exact integer atomics), hence deterministic. Work is split into chunks of
-// kChunkWords words; chunk c belongs to tensor chunk_tensor[c] and starts at word chunk_word[c].
-// HBM-bound: one read of every byte (R50: ~100 MB of fp32 weights, ~15-20 us).
+// Fingerprint of a tensor of N 32-bit words w_i: sum_i H(w_i, i) mod 2^64 with the 64-bit word hash
+// H(w, i) = fmix32(w ^ i * 0x9E3779B9) | fmix32(w ^ (i * 0x85EBCA6B + 0xC2B2AE35)) << 32 (fmix32 =
+// the MurmurHash3 finalizer, a bijection on 32-bit values). For a fixed i, H is injective in w, so
+// changing any word changes its term by a pseudo-random non-zero amount; several changed words
+// cancel with probability ~2^-64 whatever their structure. (A plain odd-multiplier sum
+// sum (w_i (2i + 1) mod 2^32) cannot see through floats with many trailing zero bits: scaling a
+// BatchNorm variance of 1.0 by 4 left it unchanged.) The sum is order-independent (exact integer
+// atomics), hence deterministic. Work is split into chunks of kChunkWords words; chunk c belongs to
+// tensor chunk_tensor[c] and starts at word chunk_word[c]. HBM-bound: one read of every byte
+// (R50: ~100 MB of fp32 weights, ~20 us; 6 quarter-rate multiplies per word stay under it).
 #include "common.h"
 
 namespace smpq {
 
 constexpr int kFpThreads = 256;
+
+__host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+__host__ __device__ __forceinline__ unsigned long long word_hash(uint32_t w, uint32_t i) {
+  const uint32_t lo = fmix32(w ^ (i * 0x9E3779B9u));
+  const uint32_t hi = fmix32(w ^ (i * 0x85EBCA6Bu + 0xC2B2AE35u));
+  return (unsigned long long)lo | ((unsigned long long)hi << 32);
+}
 constexpr long long kChunkWords = 16384;  // 64 KiB per block
 
 __global__ __launch_bounds__(kFpThreads) void fingerprint_kernel(const uint32_t* const* __restrict__ ptrs,
@@ -40,16 +58,13 @@ __global__ __launch_bounds__(kFpThreads) void fingerprint_kernel(const uint32_t*
   if (vec) {
     const uint4* q = reinterpret_cast<const uint4*>(p + w0);
     const int nq = (int)((w1 - w0) >> 2);
-    const unsigned base = (unsigned)(2 * w0 + 1);
     for (int j = threadIdx.x; j < nq; j += kFpThreads) {
       const uint4 v = q[j];
-      const unsigned m = base + 8u * (unsigned)j;  // 2i + 1 for i = w0 + 4j (mod 2^32)
-      acc += (unsigned long long)(v.x * m) + (unsigned long long)(v.y * (m + 2u)) +
-             (unsigned long long)(v.z * (m + 4u)) + (unsigned long long)(v.w * (m + 6u));
+      const uint32_t i = (uint32_t)w0 + 4u * (uint32_t)j;  // word index of v.x (tensors < 2^32 words)
+      acc += word_hash(v.x, i) + word_hash(v.y, i + 1u) + word_hash(v.z, i + 2u) + word_hash(v.w, i + 3u);
     }
   } else {
-    for (long long i = w0 + threadIdx.x; i < w1; i += kFpThreads)
-      acc += (unsigned long long)(p[i] * (unsigned)(2 * i + 1));
+    for (long long i = w0 + threadIdx.x; i < w1; i += kFpThreads) acc += word_hash(p[i], (uint32_t)i);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, kWave);
@@ -110,6 +125,6 @@ extern "C" int smpq_fingerprint_compare(const uint64_t* a, const uint64_t* b, in
 extern "C" uint64_t smpq_fingerprint_host(const void* p, int64_t nwords) {
   const uint32_t* w = static_cast<const uint32_t*>(p);
   unsigned long long acc = 0;
-  for (long long i = 0; i < nwords; ++i) acc += (unsigned long long)(w[i] * (unsigned)(2 * i + 1));
+  for (long long i = 0; i < nwords; ++i) acc += word_hash(w[i], (uint32_t)i);
   return acc;
 }

@@ -128,13 +128,13 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // scale already multiplied by 1 / (output step), code = med3(rne(z), lo, QMAX) (lo = 0 for ReLU).
 // Returns the largest rounded |z| (the overflow test: > QMAX), writes the codes' limb dwords. Both
 // LDS-DMA kernels use it, so their static-range outputs agree bit for bit.
+// lean_codes: the same, returning the clamped codes themselves (the fused stem + max pool pools
+// them before encoding).
 template <int L, int NACC, int SMIN>
-__device__ __forceinline__ float lean_quad(const v4i* accs, float rscale, const float* csq, const float* shq,
-                                           bool has_res, const int* rqv, float rsq, bool relu, float lo,
-                                           unsigned* wq) {
+__device__ __forceinline__ float lean_codes(const v4i* accs, float rscale, const float* csq, const float* shq,
+                                            bool has_res, const int* rqv, float rsq, bool relu, float lo, int* q) {
   constexpr float qmax = act_qmax<L>();
   constexpr float w0 = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
-  int q[4];
   float m = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -148,6 +148,15 @@ __device__ __forceinline__ float lean_quad(const v4i* accs, float rscale, const 
     m = fmaxf(m, relu ? zr : fabsf(zr));
     q[r] = (int)__builtin_amdgcn_fmed3f(zr, lo, qmax);
   }
+  return m;
+}
+
+template <int L, int NACC, int SMIN>
+__device__ __forceinline__ float lean_quad(const v4i* accs, float rscale, const float* csq, const float* shq,
+                                           bool has_res, const int* rqv, float rsq, bool relu, float lo,
+                                           unsigned* wq) {
+  int q[4];
+  const float m = lean_codes<L, NACC, SMIN>(accs, rscale, csq, shq, has_res, rqv, rsq, relu, lo, q);
   encode4<L>(q, wq);
   return m;
 }

@@ -93,6 +93,13 @@ __global__ __launch_bounds__(kQThreads) void quantize_channels_kernel(
 //     m = rne(w / wscale).
 //   lw == 1: m - offset stored as one int8 plane (offset != 0 only when [min m, max m] is not
 //     inside [-128, 127]); lw >= 2: m stored as lw balanced int8 digit planes, no offset.
+//   lw >= 2, exact channels: m is shifted left by the most bits that keep max|m| << sh <= WMAX
+//     (wscale = step * 2^-sh, exact), so every channel's magnitude sits in the TOP weight limb.
+//     The conv kernels skip the low-digit products (limb pairs l + lw < L + LW - 4); without the
+//     shift an 8-bit code would live in limb 0 alone and lose the low activation limbs entirely
+//     (a mixed exact / fixed-point conv of a mid-search layer was off by ~1e-3 of its logits).
+//     The shift changes no value (m * step == (m << sh) * (step * 2^-sh) exactly), only which
+//     limb products carry it.
 //   Layout: codes[l][c][k], k = tap * cin_pad + ci (tap = r * kw + q), zero-padded to K.
 //   status[0] += off-grid channels (lw == 1: error), status[1] += channels whose exact codes do
 //   not fit (lw == 1: > 256 levels), status[2] += channels coded in fixed mode.
@@ -153,6 +160,13 @@ __global__ __launch_bounds__(kQThreads) void pack_weights_ex_kernel(
     fixed = true;
     sc = amax > 0.f ? amax / wmax : 1.f;
   }
+  int sh = 0;  // lw >= 2, exact channel: normalize the codes into the top limb
+  if (lw >= 2 && !bad) {
+    const int am = max(abs(mmin), abs(mmax));
+    const int lim = (int)wmax;
+    while (am > 0 && sh < 8 * (lw - 1) && (am << (sh + 1)) <= lim) ++sh;
+    sc = ldexpf(s, -sh);
+  }
   if (threadIdx.x == 0) {
     if (bad && s > 0.f) atomicAdd(&status[0], 1);
     if (lw == 1 && bad && !(s > 0.f)) atomicAdd(&status[0], 1);
@@ -180,7 +194,7 @@ __global__ __launch_bounds__(kQThreads) void pack_weights_ex_kernel(
       const float v = row[src];
       // fixed point: round in double (at 24 bits an fp32 quotient cannot round exactly)
       if (fixed) m = (int)fmin(fmax(rint((double)v / (double)sc), -(double)wmax), (double)wmax);
-      else m = (int)rintf(__fdiv_rn(v, sc)) - o;
+      else m = ((int)rintf(__fdiv_rn(v, s)) - o) * (1 << sh);
     }
     for (int l = 0; l < lw; ++l) {  // balanced base-256 digits (the last one takes the rest)
       const int lo = (l == lw - 1) ? m : ((m + 128) & 255) - 128;

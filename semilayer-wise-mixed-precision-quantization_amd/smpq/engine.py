@@ -53,6 +53,9 @@ CHUNK = [int(_os.environ.get("SMPQ_CHUNK", "256"))]
 # replay the static-range forward from a captured HIP graph (one launch instead of ~60 kernels
 # with their Python/ctypes host cost); recaptured when weights, BN, ranges or shapes change
 USE_GRAPH = [_os.environ.get("SMPQ_GRAPH", "1") != "0"]
+# static range: conv1 + bn1 + relu + maxpool as ONE launch (ops.stem_pool_s2d; bitwise identical to
+# the stem conv followed by maxpool_limbs, without the 112x112 conv output round trip)
+FUSED_STEM = [_os.environ.get("SMPQ_FUSED_STEM", "1") != "0"]
 stats.setdefault("graph_captures", 0)
 stats.setdefault("graph_replays", 0)
 
@@ -281,6 +284,11 @@ def stem_forward(model, x, ctx=None):
         conv = model.conv1
         if ctx is not None and ctx.ranges is not None and id(conv) in ctx.ranges and conv.out_channels % 16 == 0:
             rng = ctx.ranges[id(conv)]
+            if FUSED_STEM[0] and conv.out_channels == 64 and ops.stem_pool_supported(xq, codes, x.shape[2], x.shape[3]):
+                model.conv1.last_path = "hip-fixed-s2d-pool"
+                yq = ops.stem_pool_s2d(xq, amax_in, codes, x.shape[2], x.shape[3], col_scale, col_shift,
+                                       emit_range=rng, overflow=ctx.overflow)
+                return Act(q=yq, amax=ctx.range_tensor(conv), rng=rng)
             _, yq = ops.tuned_stem_conv_s2d(xq, amax_in, codes, x.shape[2], x.shape[3], col_scale, col_shift,
                                             relu=True, emit_range=rng, overflow=ctx.overflow, want_f32=False)
             return Act(q=ops.maxpool_limbs(yq), amax=ctx.range_tensor(conv), rng=rng)
@@ -394,7 +402,7 @@ def _static_eager(model, x, cal):
 
 
 def _graph_key(model, x, cal):
-    return (tuple(x.shape), x.dtype, x.device, cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]))
+    return (tuple(x.shape), x.dtype, x.device, cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0])
 
 
 def _graph_ready(model, x, cal):

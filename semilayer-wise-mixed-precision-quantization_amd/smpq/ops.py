@@ -250,6 +250,41 @@ def tuned_stem_conv_s2d(xq, x_absmax, codes, h, w, col_scale, col_shift, relu=Tr
                          -1 if cfg is None else cfg, **kw)
 
 
+def stem_pool_supported(xq, codes, h, w):
+    """True when stem_pool_s2d handles these planes / codes (cout 64, h and w multiples of 4,
+    w <= 224, (limbs, wlimbs) in {(3, 3), (2, 2), (1, 2)})."""
+    limbs, n = xq.shape[:2]
+    wlimbs, cout = codes.shape[:2]
+    return bool(_lib.load().smpq_stem_pool_supported(n, h, w, cout, int(limbs), int(wlimbs)))
+
+
+def stem_pool_s2d(xq, x_absmax, codes, h, w, col_scale, col_shift, emit_range, overflow):
+    """conv1 7x7/2/3 + BN + ReLU + maxpool 3x3/2/1 (resnet.py:143-147) in one launch, static range:
+    the pooled output's limb planes [limbs, n, h/4, w/4, 64], bitwise identical to
+    maxpool_limbs(stem_conv_s2d(..., relu=True, emit_range=emit_range)[1])."""
+    limbs, n, h2, w2, c16 = xq.shape
+    _req(c16 == 16 and h2 * 2 == h and w2 * 2 == w, "stem_pool_s2d: planes do not match h, w")
+    wlimbs, cout, K = codes.shape
+    _req(K == 256, "stem_pool_s2d: codes must come from pack_weights_s2d")
+    _req(overflow is not None and emit_range is not None, "stem_pool_s2d: needs an output range and an overflow flag")
+    yq = torch.empty(limbs, n, h // 4, w // 4, cout, dtype=torch.int8, device=xq.device)
+    lib = _lib.load()
+    hook = _CONV_HOOK[0]
+    if hook is not None:
+        hook.begin()
+    with torch.cuda.device(xq.device):
+        _lib.check(lib.smpq_stem_pool_s2d_q(
+            _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, _lib.ptr(codes), int(wlimbs), cout, _lib.ptr(col_scale),
+            _lib.ptr(col_shift), int(limbs), _lib.ptr(yq), float(emit_range), _lib.ptr(overflow),
+            _lib.stream_ptr()), "smpq_stem_pool_s2d_q")
+    if hook is not None:
+        work = alg_work(n, h, w, 3, cout, 7, 7, h // 2, w // 2, limbs, wlimbs, False, False, False, False)
+        work["bytes"] += limbs * n * (h // 4) * (w // 4) * cout  # the pooled output, written once
+        work["shape"] = "%4d->%4d k7 %3d->%3d pool" % (3, cout, h, h // 4)
+        hook.end(work)
+    return yq
+
+
 def maxpool_limbs(xq):
     """3x3/2/1 max pool on limb planes [L, n, h, w, c] (c % 16 == 0) -> [L, n, ho, wo, c] (exact:
     the quantizer is monotone, so pooling the codes = quantizing the pooled values)."""

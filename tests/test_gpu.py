@@ -566,12 +566,43 @@ def test_pack_weights_ex_modes(gpu):
     # exact codes of quantized channels in two limbs
     wq = w.clone()
     step = ops.quantize_channels_(wq.reshape(70, -1), [8] * 70)
-    codes2, _, wscale2, st2 = ops.pack_weights_ex(wq, step, 2)
-    assert st2.cpu().tolist() == [0, 0, 0]
-    assert torch.equal(wscale2, step)
-    m2 = codes2[0].long() + 256 * codes2[1].long()
-    rec = (m2.float() * step[:, None])
-    assert torch.equal(rec.view(torch.int32), wq.permute(0, 2, 3, 1).reshape(70, -1).contiguous().view(torch.int32))
+    for lw in (2, 3):
+        codes2, _, wscale2, st2 = ops.pack_weights_ex(wq, step, lw)
+        assert st2.cpu().tolist() == [0, 0, 0]
+        m2 = sum(codes2[l].long() * 256 ** l for l in range(lw))
+        # codes normalized into the top limb: wscale = step * 2^-sh, |m| << sh <= WMAX < |m| << (sh + 1)
+        shift = torch.log2(step.double() / wscale2.double())
+        assert torch.equal(shift, shift.round()) and int(shift.min()) >= 1
+        wmax = 32512 if lw == 2 else 8323072
+        top = m2.abs().amax(1)
+        assert bool((top <= wmax).all()) and bool((2 * top > wmax).all())
+        rec = (m2.double() * wscale2.double()[:, None]).float()
+        assert torch.equal(rec.view(torch.int32), wq.permute(0, 2, 3, 1).reshape(70, -1).contiguous().view(torch.int32))
+
+
+def test_mixed_exact_fixed_conv_keeps_precision(gpu):
+    """A conv whose channels are partly exact 8-bit codes and partly fixed point (a mid-search
+    layer) takes 24-bit weight limbs; the low-digit products its kernel skips must not cost the
+    exact channels their low activation limbs (codes normalized into the top limb)."""
+    from smpq import ops
+    g = torch.Generator().manual_seed(77)
+    cin, cout, k = 64, 32, 3
+    w = (torch.randn(cout, cin, k, k, generator=g) * 0.05).to(gpu)
+    wq = w.clone()
+    bits = [8] * 16 + [0] * 16
+    step = ops.quantize_channels_(wq.reshape(cout, -1), bits)
+    codes, _, wscale, st = ops.pack_weights_ex(wq, step, 3)
+    assert st.cpu().tolist() == [0, 0, 16]
+    x = torch.relu(torch.randn(2, 12, 12, cin, generator=g)).to(gpu)
+    am = ops.act_absmax(x)
+    y = ops.conv2d_q(ops.act_quantize(x, am, 3), am, codes, None, k, k, 1, 1, wscale.contiguous(),
+                     torch.zeros(cout, device=gpu))
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).double(), wq.double(), padding=1).permute(0, 2, 3, 1)
+    scale = ref.abs().amax()
+    err_exact = ((y.double() - ref)[..., :16].abs().amax() / scale).item()
+    err_fixed = ((y.double() - ref)[..., 16:].abs().amax() / scale).item()
+    assert err_exact < 1e-6, err_exact  # was ~2e-3 with the codes in the low limb
+    assert err_fixed < 5e-5, err_fixed  # 24-bit fixed point, skipped low-digit products
 
 
 @pytest.mark.parametrize("limbs,wlimbs", [(1, 2), (2, 2), (3, 2), (3, 3)])
@@ -667,7 +698,7 @@ def test_stem_s2d_bitwise_matches_4ch_stem(gpu, limbs, hw):
     ovf4 = torch.zeros(1, dtype=torch.int32, device=gpu)
     _, yq4 = ops.conv2d_q(ops.image_quantize(x, am, limbs), am, codes4, None, 7, 7, 2, 3, cs, sh, relu=True,
                           emit_range=rng, overflow=ovf4, want_f32=False)
-    tried = 0
+    tried, yq0 = 0, None
     for c in ops.tile_configs():
         if ops.tile_kind(c) != ops.TILE_LDS_DMA:
             continue
@@ -682,9 +713,16 @@ def test_stem_s2d_bitwise_matches_4ch_stem(gpu, limbs, hw):
         ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
         _, yq = ops.stem_conv_s2d(xs, am, codes16, h, w, cs, sh, relu=True, tile_cfg=c, emit_range=rng,
                                   overflow=ovf, want_f32=False)
-        assert torch.equal(yq, yq4), c
+        # limb planes only: the s2d stem takes the lean static epilogue (1/step folded into the
+        # column scale), identical across its tiles and within a code unit or two of the general
+        # epilogue's (test_lean_static_epilogue)
+        yq0 = yq if yq0 is None else yq0
+        assert torch.equal(yq, yq0), c
         assert int(ovf.item()) == 0 == int(ovf4.item())
     assert tried >= 3
+    lean = sum(yq0[l].cpu().numpy().astype(np.int64) * 256 ** l for l in range(limbs))
+    full = sum(yq4[l].cpu().numpy().astype(np.int64) * 256 ** l for l in range(limbs))
+    assert np.abs(lean - full).max() <= (1 if limbs == 2 else 2)
 
 
 @pytest.mark.parametrize("limbs", [1, 2, 3])
@@ -698,6 +736,62 @@ def test_maxpool_limbs_equals_quantized_maxpool(gpu, limbs):
     xq = ops.act_quantize(x, rng, limbs)
     pooled = F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1).contiguous()
     assert torch.equal(ops.maxpool_limbs(xq), ops.act_quantize(pooled, rng, limbs))
+
+
+@pytest.mark.parametrize("limbs", [1, 2, 3])
+@pytest.mark.parametrize("nhw", [(2, 224, 224), (3, 40, 36), (1, 32, 64), (2, 100, 220)])
+def test_fused_stem_pool_bitwise(gpu, limbs, nhw):
+    """conv1 + bn1 + relu + maxpool in one launch == stem_conv_s2d (static range) + maxpool_limbs,
+    bit for bit: every workgroup band split (2 images -> one pooled row per band at 224; 1 image ->
+    16 bands), partial column fragments (w/2 = 18, 110), and the overflow flag with a range that
+    clamps."""
+    from smpq import ops
+    n, h, w = nhw
+    g = torch.Generator().manual_seed(31 + limbs + h)
+    wt = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(gpu)
+    x = torch.randn(n, 3, h, w, generator=g).to(gpu)
+    x[0] *= 3.0
+    am = ops.act_absmax(x)
+    lw = max(2, limbs)
+    codes, wscale = ops.pack_weights_s2d(wt, lw)
+    cs = (wscale * torch.linspace(0.5, 2, 64, device=gpu)).contiguous()
+    sh = torch.linspace(-1, 1, 64, device=gpu).contiguous()
+    xs = ops.image_quantize_s2d(x, am, limbs)
+    assert ops.stem_pool_supported(xs, codes, h, w)
+    ya = torch.zeros(n, device=gpu)
+    y = ops.stem_conv_s2d(xs, am, codes, h, w, cs, sh, relu=True, y_absmax=ya)
+    for frac, want_ovf in ((1.5, 0), (0.3, 1)):
+        rng = float(y.abs().max()) * frac
+        o2 = torch.zeros(1, dtype=torch.int32, device=gpu)
+        _, yq = ops.stem_conv_s2d(xs, am, codes, h, w, cs, sh, relu=True, emit_range=rng, overflow=o2,
+                                  want_f32=False)
+        ref = ops.maxpool_limbs(yq)
+        o1 = torch.zeros(1, dtype=torch.int32, device=gpu)
+        got = ops.stem_pool_s2d(xs, am, codes, h, w, cs, sh, emit_range=rng, overflow=o1)
+        assert got.shape == ref.shape == (limbs, n, h // 4, w // 4, 64)
+        assert torch.equal(got, ref), (frac, (got != ref).sum().item())
+        assert int(o1.item()) == int(o2.item()) == want_ovf
+
+
+def test_fused_stem_in_the_model(gpu):
+    """The static-range forward with the fused stem gives the same logits as with the two-launch
+    stem (eager and graph replay)."""
+    from smpq import engine
+    net = build_model(gpu, "resnet50", "r50_mixed")
+    x = torch.randn(4, 3, 224, 224, generator=torch.Generator().manual_seed(17)).to(gpu)
+    old = engine.FUSED_STEM[0]
+    try:
+        with torch.no_grad():
+            engine.FUSED_STEM[0] = False
+            net(x)  # calibrate
+            a = net(x)
+            engine.FUSED_STEM[0] = True
+            b = net(x)
+            c = net(x)
+        assert net.conv1.last_path == "hip-fixed-s2d-pool"
+    finally:
+        engine.FUSED_STEM[0] = old
+    assert torch.equal(a, b) and torch.equal(a, c)
 
 
 @pytest.mark.parametrize("limbs", [2, 3])

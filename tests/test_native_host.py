@@ -151,13 +151,25 @@ def test_imagenet_synthetic_is_opt_in(monkeypatch):
 
 
 def test_host_fingerprint_formula(built_lib):
-    # smpq_fingerprint_host = sum_i ((w_i * (2i + 1)) mod 2^32) mod 2^64 (the device kernel's formula)
+    # smpq_fingerprint_host = sum_i H(w_i, i) mod 2^64 (the device kernel's formula, include/smpq.h)
     from smpq.fingerprint import host_fingerprint
+    M = (1 << 32) - 1
+
+    def fmix32(h):
+        h ^= h >> 16
+        h = (h * 0x85EBCA6B) & M
+        h ^= h >> 13
+        h = (h * 0xC2B2AE35) & M
+        return h ^ (h >> 16)
+
     t = torch.randn(1000, generator=torch.Generator().manual_seed(3))
-    w = t.numpy().view(np.uint32).astype(np.uint64)
-    prod = (w * (2 * np.arange(1000, dtype=np.uint64) + 1)) % (1 << 32)
-    exp = int(prod.sum(dtype=np.uint64))
+    w = t.numpy().view(np.uint32).tolist()
+    exp = sum(fmix32(x ^ ((i * 0x9E3779B9) & M)) | (fmix32(x ^ ((i * 0x85EBCA6B + 0xC2B2AE35) & M)) << 32)
+              for i, x in enumerate(w)) % (1 << 64)
     assert host_fingerprint(t) == exp
     t2 = t.clone()
     t2[999] = torch.nextafter(t2[999], torch.tensor(1e9))
     assert host_fingerprint(t2) != exp
+    # structured change the old odd-multiplier sum missed: a BN variance of ones scaled by 4
+    ones = torch.ones(128)
+    assert host_fingerprint(ones) != host_fingerprint(ones * 4.0)
