@@ -51,7 +51,7 @@ constexpr int kAblate = SMPQ_DIAG_ABLATE;
 // scale / shift and the residual scale, ReLU and the code clamp are one v_med3, and overflow is
 // tracked on the rounded codes — about half the VALU work of the general epilogue per output.
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
-          bool LEAN = false>
+          bool LEAN = false, bool PIPE = false>
 __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kernel(ConvArgs a) {
   static_assert(BK == 64 || BK == 128, "BK");
   static_assert(!S2D || BK == 64, "the s2d stem uses 64-B K steps");
@@ -83,6 +83,7 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __builtin_assume(wave >= 0 && wave < NW);
   const int wc = wave / WAVES_P, wp = wave % WAVES_P;
 
   // ---- XCD-aware tile order ----------------------------------------------------------------
@@ -283,12 +284,17 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
                                                                                   (unsigned)((long long)l * oplane), 0);
   }
 
-  // DMA pieces this wave issues per K step (wave-uniform): the counted vmcnt below
+  // DMA pieces this wave issues per K step (wave-uniform): the counted vmcnt below. When the
+  // pieces divide evenly over the waves the count is a compile-time constant (PPW) and so are the
+  // steady-state waits.
+  constexpr bool kUniform = (WPIECES % NW) == 0 && (APIECES % NW) == 0;
+  constexpr int PPW = (WPIECES + APIECES) / NW;
   int ppw = 0;
 #pragma unroll
   for (int s = 0; s < WSLOTS; ++s) ppw += (wave + NW * s < WPIECES) ? 1 : 0;
 #pragma unroll
   for (int s = 0; s < ASLOTS; ++s) ppw += (wave + NW * s < APIECES) ? 1 : 0;
+  if constexpr (kUniform) ppw = PPW;
 
   int kr = 0, kc = 0, c0 = 0;  // K position of the next step to issue
   auto advance = [&]() {
@@ -302,84 +308,145 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
     }
   };
   int nissued = 0, wbuf = 0, rbuf = 0;
+  // fragments of one MFMA K step of a stage
+  struct Frags {
+    v4i w[LW][WC], a[L][WP];
+  };
+  auto read_frags = [&](Frags& f, const int8_t* sb, int h) {
 #pragma unroll
-  for (int st = 0; st < NST - 1; ++st) {
-    if (st < nsteps) {
-      issue(wbuf, kr, kc, c0, st);
-      advance();
-      ++nissued;
-      wbuf = wbuf + 1 == NST ? 0 : wbuf + 1;
-    }
-  }
-  for (int ks = 0; ks < nsteps; ++ks) {
-    // this wave's DMA of step ks has landed (the younger steps' may still fly) and its reads of
-    // step ks-1 are done; after the barrier every wave's are, so stage ks is readable and the
-    // stage of step ks-1 may be refilled
-    if constexpr (NST == 2) {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    } else {
-      wait_vmcnt((nissued - ks - 1) * ppw);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const int8_t* sb = lds + rbuf * STAGE;
-    rbuf = rbuf + 1 == NST ? 0 : rbuf + 1;
-    // fragments of MFMA K step h of this stage (the DMA below writes the other stage, so the second
-    // half may be read after the first half's MFMAs: half the fragment registers live at a time)
-    v4i wf[LW][WC], af[L][WP];
-    auto read_frags = [&](int h) {
+    for (int lw = 0; lw < LW; ++lw)
 #pragma unroll
-      for (int lw = 0; lw < LW; ++lw)
+      for (int i = 0; i < WC; ++i)
+        f.w[lw][i] = *reinterpret_cast<const v4i*>(sb + (lw * BC + (wc * WC + i) * 16) * BK + rd[h]);
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+#pragma unroll
+      for (int j = 0; j < WP; ++j)
+        f.a[l][j] = *reinterpret_cast<const v4i*>(sb + WPIECES * 1024 + (l * BP + (wp * WP + j) * 16) * BK + rd[h]);
+  };
+  auto mma = [&](const Frags& f) {
+    if (do_off) {
+#pragma unroll
+      for (int l = 0; l < L; ++l)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+          int s = rs[l][j];
+          s = __builtin_amdgcn_sdot4(f.a[l][j].x, 0x01010101, s, false);
+          s = __builtin_amdgcn_sdot4(f.a[l][j].y, 0x01010101, s, false);
+          s = __builtin_amdgcn_sdot4(f.a[l][j].z, 0x01010101, s, false);
+          s = __builtin_amdgcn_sdot4(f.a[l][j].w, 0x01010101, s, false);
+          rs[l][j] = s;
+        }
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+#pragma unroll
+      for (int lw = 0; lw < LW; ++lw) {
+        if (l + lw < SMIN || (kAblate & 8)) continue;  // compile-time: skipped low-digit product
 #pragma unroll
         for (int i = 0; i < WC; ++i)
-          wf[lw][i] = *reinterpret_cast<const v4i*>(sb + (lw * BC + (wc * WC + i) * 16) * BK + rd[h]);
 #pragma unroll
-      for (int l = 0; l < L; ++l)
-#pragma unroll
-        for (int j = 0; j < WP; ++j)
-          af[l][j] = *reinterpret_cast<const v4i*>(sb + WPIECES * 1024 + (l * BP + (wp * WP + j) * 16) * BK + rd[h]);
-    };
-    auto mma = [&]() {
-      if (do_off) {
-#pragma unroll
-        for (int l = 0; l < L; ++l)
-#pragma unroll
-          for (int j = 0; j < WP; ++j) {
-            int s = rs[l][j];
-            s = __builtin_amdgcn_sdot4(af[l][j].x, 0x01010101, s, false);
-            s = __builtin_amdgcn_sdot4(af[l][j].y, 0x01010101, s, false);
-            s = __builtin_amdgcn_sdot4(af[l][j].z, 0x01010101, s, false);
-            s = __builtin_amdgcn_sdot4(af[l][j].w, 0x01010101, s, false);
-            rs[l][j] = s;
-          }
+          for (int j = 0; j < WP; ++j)
+            acc[l + lw - SMIN][i][j] =
+                __builtin_amdgcn_mfma_i32_16x16x64_i8(f.w[lw][i], f.a[l][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int l = 0; l < L; ++l)
-#pragma unroll
-        for (int lw = 0; lw < LW; ++lw) {
-          if (l + lw < SMIN || (kAblate & 8)) continue;  // compile-time: skipped low-digit product
-#pragma unroll
-          for (int i = 0; i < WC; ++i)
-#pragma unroll
-            for (int j = 0; j < WP; ++j)
-              acc[l + lw - SMIN][i][j] =
-                  __builtin_amdgcn_mfma_i32_16x16x64_i8(wf[lw][i], af[l][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
-        }
-    };
-    read_frags(0);
-    // start the DMA of step ks + NST - 1 into the stage step ks - 1 used
+  };
+  auto issue_next = [&]() {
     if (nissued < nsteps) {
       issue(wbuf, kr, kc, c0, nissued);
       advance();
       ++nissued;
       wbuf = wbuf + 1 == NST ? 0 : wbuf + 1;
     }
-    mma();
+  };
+  // wait until this wave's DMA of step `ready` has landed (younger steps may still fly)
+  auto wait_step = [&](int ready) {
+    const int d = nissued - ready - 1;  // steps issued after it
+    if (kUniform && d == NST - 1) {
+      wait_vm<PPW * (NST - 1)>();
+    } else if (kUniform && d == NST - 2) {
+      wait_vm<PPW * (NST - 2)>();
+    } else {
+      wait_vmcnt(d * ppw);
+    }
+  };
+
+  if constexpr (PIPE) {
+    // Register-pipelined K loop (two fragment register sets): after the barrier that certifies
+    // stage ks + 1 (every wave's DMA of it landed, every wave's reads of stage ks done — waited
+    // before the barrier), the first fragments of step ks + 1 are read while step ks's MFMAs run
+    // from registers, and the DMA of step ks + NST refills stage ks. The MFMAs never wait on LDS.
+    // KH == 1: the two sets alternate between steps; KH == 2: set X holds the first MFMA K step of
+    // a stage, set Y the second (read from the same stage before X's MFMAs).
 #pragma unroll
-    for (int h = 1; h < KH; ++h) {
-      read_frags(h);
-      mma();
+    for (int st = 0; st < NST; ++st)
+      if (st < nsteps) issue_next();
+    Frags fx, fy;
+    wait_step(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int8_t* sb = lds;
+    read_frags(fx, sb, 0);
+    rbuf = 1 == NST ? 0 : 1;
+    auto next_stage = [&](int ks, Frags& f) {  // barrier for stage ks + 1, read its first fragments
+      wait_step(ks + 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      sb = lds + rbuf * STAGE;
+      rbuf = rbuf + 1 == NST ? 0 : rbuf + 1;
+      read_frags(f, sb, 0);
+      issue_next();  // into the stage of step ks
+    };
+    if constexpr (KH == 1) {
+      auto step = [&](int ks, Frags& cur, Frags& nxt) {
+        if (ks + 1 < nsteps) next_stage(ks, nxt);
+        mma(cur);
+      };
+      for (int ks = 0; ks < nsteps; ks += 2) {
+        step(ks, fx, fy);
+        if (ks + 1 < nsteps) step(ks + 1, fy, fx);
+      }
+    } else {
+      static_assert(KH == 2, "KH");
+      for (int ks = 0; ks < nsteps; ++ks) {
+        read_frags(fy, sb, 1);
+        mma(fx);
+        if (ks + 1 < nsteps) next_stage(ks, fx);
+        mma(fy);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  } else {
+#pragma unroll
+    for (int st = 0; st < NST - 1; ++st)
+      if (st < nsteps) issue_next();
+    for (int ks = 0; ks < nsteps; ++ks) {
+      // this wave's DMA of step ks has landed (the younger steps' may still fly) and its reads of
+      // step ks-1 are done; after the barrier every wave's are, so stage ks is readable and the
+      // stage of step ks-1 may be refilled
+      if constexpr (NST == 2) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      } else {
+        wait_step(ks);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int8_t* sb = lds + rbuf * STAGE;
+      rbuf = rbuf + 1 == NST ? 0 : rbuf + 1;
+      // fragments of MFMA K step h of this stage (the DMA below writes the other stage, so the
+      // second half may be read after the first half's MFMAs: half the fragment registers live)
+      Frags f;
+      read_frags(f, sb, 0);
+      issue_next();  // the DMA of step ks + NST - 1 into the stage step ks - 1 used
+      mma(f);
+#pragma unroll
+      for (int h = 1; h < KH; ++h) {
+        read_frags(f, sb, h);
+        mma(f);
+      }
     }
   }
 
@@ -679,43 +746,55 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 
 // ------------------------------------------------------------------------------------------
 struct GldsCfg {
-  int wavesc, wavesp, wc, wp, stages, bk;
+  int wavesc, wavesp, wc, wp, stages, bk, pipe;
 };
 constexpr GldsCfg kGlds[] = {
-    {2, 2, 2, 2, 2, 64},  // 0:  64 ch x  64 px, 256 threads
-    {2, 2, 2, 4, 2, 64},  // 1:  64 ch x 128 px
-    {2, 2, 4, 2, 2, 64},  // 2: 128 ch x  64 px
-    {1, 4, 4, 1, 2, 64},  // 3:  64 ch x  64 px (each wave all 64 channels of 16 px)
-    {1, 4, 4, 2, 2, 64},  // 4:  64 ch x 128 px
-    {4, 1, 2, 4, 2, 64},  // 5: 128 ch x  64 px (each wave 32 ch x all 64 px)
-    {2, 2, 4, 4, 2, 64},  // 6: 128 ch x 128 px (<= 2 accumulator sets)
-    {4, 1, 4, 2, 2, 64},  // 7: 256 ch x  32 px (whole 256-B output rows per block: wide 1x1 expansions)
-    {4, 1, 4, 1, 2, 64},  // 8: 256 ch x  16 px
-    {2, 2, 4, 1, 2, 64},  // 9: 128 ch x  32 px
-    {2, 2, 2, 2, 3, 64},  // 10: as 0, 3 LDS stages (DMA two K steps ahead; long-K 3x3 convs)
-    {1, 4, 4, 1, 3, 64},  // 11: as 3, 3 stages
-    {2, 2, 4, 2, 3, 64},  // 12: as 2, 3 stages
+    {2, 2, 2, 2, 2, 64, 0},  // 0:  64 ch x  64 px, 256 threads
+    {2, 2, 2, 4, 2, 64, 0},  // 1:  64 ch x 128 px
+    {2, 2, 4, 2, 2, 64, 0},  // 2: 128 ch x  64 px
+    {1, 4, 4, 1, 2, 64, 0},  // 3:  64 ch x  64 px (each wave all 64 channels of 16 px)
+    {1, 4, 4, 2, 2, 64, 0},  // 4:  64 ch x 128 px
+    {4, 1, 2, 4, 2, 64, 0},  // 5: 128 ch x  64 px (each wave 32 ch x all 64 px)
+    {2, 2, 4, 4, 2, 64, 0},  // 6: 128 ch x 128 px (<= 2 accumulator sets)
+    {4, 1, 4, 2, 2, 64, 0},  // 7: 256 ch x  32 px (whole 256-B output rows per block: wide 1x1 expansions)
+    {4, 1, 4, 1, 2, 64, 0},  // 8: 256 ch x  16 px
+    {2, 2, 4, 1, 2, 64, 0},  // 9: 128 ch x  32 px
+    {2, 2, 2, 2, 3, 64, 0},  // 10: as 0, 3 LDS stages (DMA two K steps ahead; long-K 3x3 convs)
+    {1, 4, 4, 1, 3, 64, 0},  // 11: as 3, 3 stages
+    {2, 2, 4, 2, 3, 64, 0},  // 12: as 2, 3 stages
     // 8 waves: twice the MFMA work per loaded byte (the 3x3 convs stream ~100 ops/B from L2 at 64 x 64)
-    {2, 4, 4, 2, 2, 64},  // 13: 128 ch x 128 px (waves 64 ch x 32 px)
-    {4, 2, 2, 4, 2, 64},  // 14: 128 ch x 128 px (waves 32 ch x 64 px)
-    {4, 2, 4, 2, 2, 64},  // 15: 256 ch x  64 px
+    {2, 4, 4, 2, 2, 64, 0},  // 13: 128 ch x 128 px (waves 64 ch x 32 px)
+    {4, 2, 2, 4, 2, 64, 0},  // 14: 128 ch x 128 px (waves 32 ch x 64 px)
+    {4, 2, 4, 2, 2, 64, 0},  // 15: 256 ch x  64 px
     // (64 ch x 256 px with 8 pixel-waves was removed: never the fastest, and its static-range
     // limb output was intermittently wrong in the last pixel group — see tests/test_gpu.py
     // test_tile_configs_deterministic)
     // 128-B K steps (cin % 128 == 0): DMA pieces of whole cache lines
-    {2, 2, 2, 2, 2, 128},  // 16: as 0
-    {1, 4, 4, 1, 2, 128},  // 17: as 3
-    {2, 2, 4, 2, 2, 128},  // 18: as 2
-    {2, 2, 4, 1, 2, 128},  // 19: as 9
-    {1, 4, 4, 2, 2, 128},  // 20: as 4
-    {2, 4, 4, 2, 2, 128},  // 21: as 13
+    {2, 2, 2, 2, 2, 128, 0},  // 16: as 0
+    {1, 4, 4, 1, 2, 128, 0},  // 17: as 3
+    {2, 2, 4, 2, 2, 128, 0},  // 18: as 2
+    {2, 2, 4, 1, 2, 128, 0},  // 19: as 9
+    {1, 4, 4, 2, 2, 128, 0},  // 20: as 4
+    {2, 4, 4, 2, 2, 128, 0},  // 21: as 13
     // deeper DMA pipelines for the long-K 3x3 convs (latency of a K step's pieces hidden behind
     // NST - 1 steps of MFMAs)
-    {2, 2, 4, 2, 4, 64},   // 22: as 2, 4 stages
-    {2, 2, 2, 2, 4, 64},   // 23: as 0, 4 stages
-    {1, 4, 4, 1, 4, 64},   // 24: as 3, 4 stages
-    {2, 2, 4, 2, 3, 128},  // 25: as 18, 3 stages
-    {2, 2, 2, 2, 3, 128},  // 26: as 16, 3 stages
+    {2, 2, 4, 2, 4, 64, 0},   // 22: as 2, 4 stages
+    {2, 2, 2, 2, 4, 64, 0},   // 23: as 0, 4 stages
+    {1, 4, 4, 1, 4, 64, 0},   // 24: as 3, 4 stages
+    {2, 2, 4, 2, 3, 128, 0},  // 25: as 18, 3 stages
+    {2, 2, 2, 2, 3, 128, 0},  // 26: as 16, 3 stages
+    // register-pipelined K loops (PIPE: two fragment register sets, the next step's fragments read
+    // under the current step's MFMAs): long-K convs; they cost registers the short-K ones need
+    {2, 2, 4, 2, 2, 64, 1},   // 27: as 2
+    {1, 4, 4, 1, 2, 64, 1},   // 28: as 3
+    {2, 2, 4, 1, 2, 64, 1},   // 29: as 9
+    {1, 4, 4, 1, 3, 64, 1},   // 30: as 11
+    {2, 2, 4, 2, 3, 64, 1},   // 31: as 12
+    {2, 2, 4, 2, 2, 128, 1},  // 32: as 18
+    {2, 2, 4, 1, 2, 128, 1},  // 33: as 19
+    {2, 2, 4, 2, 4, 64, 1},   // 34: as 22
+    {1, 4, 4, 1, 4, 64, 1},   // 35: as 24
+    {2, 2, 2, 2, 3, 128, 1},  // 36: as 26
 };
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
@@ -750,7 +829,7 @@ void glds_cfg_info(int cfg, int* bm, int* bn, int* threads) {
 }
 
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, bool S2D = false, int NST = 2, int MINW = 2,
-          int BK = 64>
+          int BK = 64, bool PIPE = false>
 static int launch_one(const ConvArgs& a, hipStream_t stream) {
   constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
   if constexpr ((L + LW - 1 - SMIN) * WC * WP * 4 > 128) {
@@ -778,8 +857,8 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
     ConvArgs b = a;
     fast_div_init((int)nt, b.ntc_mul, b.ntc_shr);
     const bool lean = L >= 2 && a.yq && !a.y && !a.residual && !a.y_absmax;
-    auto kfull = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, false>;
-    auto klean = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, (L >= 2)>;
+    auto kfull = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, false, PIPE>;
+    auto klean = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, (L >= 2), PIPE>;
     auto set_lds = [](const void* k) {
       const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                kMaxNeed < kMaxLds ? kMaxNeed : kMaxLds);
@@ -826,6 +905,16 @@ static int launch_cfg(int cfg, const ConvArgs& a, hipStream_t s) {
     case 24: return launch_one<L, LW, 1, 4, 4, 1, false, 4>(a, s);
     case 25: return launch_one<L, LW, 2, 2, 4, 2, false, 3, 2, 128>(a, s);
     case 26: return launch_one<L, LW, 2, 2, 2, 2, false, 3, 2, 128>(a, s);
+    case 27: return launch_one<L, LW, 2, 2, 4, 2, false, 2, 2, 64, true>(a, s);
+    case 28: return launch_one<L, LW, 1, 4, 4, 1, false, 2, 2, 64, true>(a, s);
+    case 29: return launch_one<L, LW, 2, 2, 4, 1, false, 2, 2, 64, true>(a, s);
+    case 30: return launch_one<L, LW, 1, 4, 4, 1, false, 3, 2, 64, true>(a, s);
+    case 31: return launch_one<L, LW, 2, 2, 4, 2, false, 3, 2, 64, true>(a, s);
+    case 32: return launch_one<L, LW, 2, 2, 4, 2, false, 2, 2, 128, true>(a, s);
+    case 33: return launch_one<L, LW, 2, 2, 4, 1, false, 2, 2, 128, true>(a, s);
+    case 34: return launch_one<L, LW, 2, 2, 4, 2, false, 4, 2, 64, true>(a, s);
+    case 35: return launch_one<L, LW, 1, 4, 4, 1, false, 4, 2, 64, true>(a, s);
+    case 36: return launch_one<L, LW, 2, 2, 2, 2, false, 3, 2, 128, true>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   }
 }

@@ -163,6 +163,12 @@ __device__ __forceinline__ float lean_quad(const v4i* accs, float rscale, const 
 
 }  // namespace
 
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant)
 __device__ __forceinline__ void wait_vmcnt(int n) {
   switch (n) {
