@@ -16,7 +16,9 @@ captured HIP graph. HIP events recorded inside a graph capture cannot be timed o
 (elapsed_time -> hipErrorInvalidHandle, tools/probe_graph_events.py), so the per-launch
 kernel durations come from a second region run right after the timed one: the same forward
 launched eagerly (the same kernels the graph replays) with HIP events around every conv
-launch on the stream it is launched on. The roofline is SURVEY.md 8(d)'s: per launch
+launch on the stream it is launched on, one launch at a time (the graph runs each stage's
+downsample conv on a side stream beside conv1/conv2; the roofline region runs it serially so
+that each event pair times one kernel alone). The roofline is SURVEY.md 8(d)'s: per launch
 T_roof = max(2 MACs / P_int8, bytes / BW_HBM) with ops/ops.alg_work's algorithmic bytes.
 """
 import argparse
@@ -183,6 +185,8 @@ def main():
     ap.add_argument("--layers", action="store_true", help="print a per-launch roofline table (stderr)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--chunk", type=int, default=None, help="images per pass (Infinity-Cache blocking)")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="batch slices run concurrently on their own streams (default: engine.STREAMS)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -207,6 +211,8 @@ def main():
     from smpq import engine
     if args.chunk:
         engine.set_chunk(args.chunk)
+    if args.streams:
+        engine.STREAMS[0] = args.streams
     torch.manual_seed(0)
     net = getattr(resnet, arch)().to(dev).eval()
     assignments.apply_assignment(net, assign)
@@ -246,8 +252,10 @@ def main():
 
     # per-launch kernel times for the roofline: the same forward, launched eagerly
     timer = ConvTimer()
-    use_graph = engine.USE_GRAPH[0]
+    use_graph, conc, nst = engine.USE_GRAPH[0], engine.CONCURRENT_DS[0], engine.STREAMS[0]
     engine.USE_GRAPH[0] = False
+    engine.CONCURRENT_DS[0] = False  # one launch at a time: events time each kernel alone
+    engine.STREAMS[0] = 1
     ops.set_conv_hook(timer)
     step()  # untimed: the eager path's first pass
     timer.active = True
@@ -255,7 +263,7 @@ def main():
         step()
     timer.active = False
     ops.set_conv_hook(None)
-    engine.USE_GRAPH[0] = use_graph
+    engine.USE_GRAPH[0], engine.CONCURRENT_DS[0], engine.STREAMS[0] = use_graph, conc, nst
     roof = timer.roofline(args.roofline_steps)
     if args.layers and rank == 0:
         timer.print_layers(args.roofline_steps)
@@ -284,7 +292,9 @@ def main():
                        "act_code": {1: "int8", 2: "int16 (2 int8 limbs)", 3: "int24 (3 int8 limbs)"}[args.limbs],
                        "parallelism": "dp%d" % world, "quantized_convs_per_step": roof["launches_per_step"],
                        "range_mode": engine.get_range_mode(), "chunk": engine.CHUNK[0],
-                       "hip_graph": bool(engine.USE_GRAPH[0])},
+                       "hip_graph": bool(engine.USE_GRAPH[0]),
+                       "concurrent_downsample": bool(engine.CONCURRENT_DS[0]),
+                       "batch_slices_on_streams": engine.STREAMS[0]},
             "roofline": roof,
         }
         if not args.no_cpu_baseline and world == 1:

@@ -56,6 +56,10 @@ USE_GRAPH = [_os.environ.get("SMPQ_GRAPH", "1") != "0"]
 # static range: conv1 + bn1 + relu + maxpool as ONE launch (ops.stem_pool_s2d; bitwise identical to
 # the stem conv followed by maxpool_limbs, without the 112x112 conv output round trip)
 FUSED_STEM = [_os.environ.get("SMPQ_FUSED_STEM", "1") != "0"]
+# static range: the downsample branch of a block runs on a side stream beside conv1 / conv2
+CONCURRENT_DS = [_os.environ.get("SMPQ_CONCURRENT_DS", "1") != "0"]
+# static range: the batch split into this many slices, each on its own stream (concurrent kernels)
+STREAMS = [int(_os.environ.get("SMPQ_STREAMS", "1"))]
 stats.setdefault("graph_captures", 0)
 stats.setdefault("graph_replays", 0)
 
@@ -148,6 +152,7 @@ class Ctx:
         # [0] a value exceeded its static range, [1] cached weight content is stale (fingerprint)
         self.overflow = torch.zeros(2, dtype=torch.int32, device=device) if ranges else None
         self._rt = cache if cache is not None else {}
+        self.lane = None                # batch slice being enqueued (its own streams)
 
     def range_tensor(self, conv):
         key = (id(conv), self.n)
@@ -213,26 +218,68 @@ def run_conv(conv, bn, act, relu, residual=None, want_amax=True, ctx=None, want_
     return Act(f32=y, amax=yam)
 
 
+_STREAMS = {}
+
+
+def _stream(key):
+    """A side stream per key (created once; reused by every forward and graph capture)."""
+    s = _STREAMS.get(key)
+    if s is None:
+        s = _STREAMS[key] = torch.cuda.Stream(device=key[0])
+    return s
+
+
+def _side_stream(device, lane):
+    """The downsample branch's stream of batch slice ``lane`` (None: the unsliced forward)."""
+    return _stream((device, "ds", lane))
+
+
 def block_forward(blk, x, ctx=None, last=False):
     """One BasicBlock / Bottleneck on an Act; returns the output Act. In static mode no
     activation is stored in fp32 except the downsample's identity and the last block's output
-    (avgpool): the identity of a block without downsample is read from its input's limb planes."""
+    (avgpool): the identity of a block without downsample is read from its input's limb planes.
+
+    Static mode: the downsample branch (resnet.py:188-192) depends only on the block input, so it
+    runs on a side stream concurrently with conv1 (and conv2) and joins before the conv that adds
+    it (fork/join inside the captured graph); every launch computes exactly what it computes
+    serially, so the result is bitwise the same (tests/test_gpu.py)."""
+    side = None
+    # (not inside a batch slice: a fork nested in a slice's fork crashes hipStreamEndCapture on
+    # ROCm 7.2 / torch 2.10 — tools/debug_streams.py recap_ds_sl)
+    if blk.downsample is not None and CONCURRENT_DS[0] and ctx is not None and ctx.ranges is not None \
+            and ctx.lane is None and x.q is not None:  # both branches read the input's limb planes
+        main = torch.cuda.current_stream()
+        side = _side_stream(x.q.device, ctx.lane)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            # allocated on the side stream, consumed on main after the join; freed blocks are
+            # reused by the side stream only after its next wait on main (the next fork), which
+            # is ordered after every consumer, so no record_stream is needed (none in a capture)
+            ds = run_conv(blk.downsample[0], blk.downsample[1], x, relu=False, ctx=ctx, want_f32=False)
+    elif blk.downsample is not None:
+        ds = run_conv(blk.downsample[0], blk.downsample[1], x, relu=False, ctx=ctx, want_f32=False)
     if blk.downsample is not None:
         # static mode: the identity as calibrated-range limb planes (3 B/element instead of fp32)
-        ds = run_conv(blk.downsample[0], blk.downsample[1], x, relu=False, ctx=ctx, want_f32=False)
         identity = ds if (ds.f32 is None and ds.q is not None and ds.rng is not None) else ds.f32
     elif x.f32 is not None or x.q is None or x.rng is None:
         identity = x.f32
     else:
         identity = x
     out_amax = not last  # the last block feeds only avgpool
+
+    def join():
+        if side is not None:
+            torch.cuda.current_stream().wait_stream(side)
+
     if hasattr(blk, "conv3"):  # Bottleneck (resnet.py:97-116)
         t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
         t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
+        join()
         return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax,
                         want_f32=last)
     # BasicBlock (resnet.py:55-68)
     t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
+    join()
     return run_conv(blk.conv2, blk.bn2, t1, True, residual=identity, ctx=ctx, want_amax=out_amax,
                     want_f32=last)
 
@@ -318,24 +365,50 @@ def _blocks(model):
     return [b for layer in (model.layer1, model.layer2, model.layer3, model.layer4) for b in layer]
 
 
-def _features(model, x, ctx):
+def _features(model, x, ctx, pool=True):
     act = stem_forward(model, x, ctx)
     blocks = _blocks(model)
     for i, blk in enumerate(blocks):
         act = block_forward(blk, act, ctx, last=(i == len(blocks) - 1))
-    return act.f32.mean(dim=(1, 2))
+    return act.f32.mean(dim=(1, 2)) if pool else act.f32
 
 
 def _forward(model, x, ctx):
     n = x.shape[0]
     c = CHUNK[0]
-    if n <= c:
+    parts = [(s, min(n, s + c)) for s in range(0, n, c)]
+    nst = STREAMS[0] if (ctx is not None and ctx.ranges is not None) else 1
+    if nst > 1 and len(parts) == 1 and n >= 2 * nst:
+        # static mode: the batch as nst concurrent slices, each on its own stream, so that one
+        # slice's bandwidth-bound convs overlap another's MFMA/L2-bound ones; every image's result
+        # is the same as in the serial forward (per-layer ranges are fixed, kernels exact)
+        step = (n + nst - 1) // nst
+        parts = [(s, min(n, s + step)) for s in range(0, n, step)]
+        main = torch.cuda.current_stream()
+        for s0, s1 in parts:  # shared per-layer range tensors exist before the fork
+            ctx.n = s1 - s0
+            for m in model.modules():
+                if id(m) in ctx.ranges:
+                    ctx.range_tensor(m)
+        feats = []
+        for i, (s0, s1) in enumerate(parts):
+            st = _stream((x.device, "slice", i))
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                ctx.n, ctx.lane = s1 - s0, i
+                feats.append(_features(model, x[s0:s1], ctx, pool=False))
+        for i in range(len(parts)):
+            main.wait_stream(_stream((x.device, "slice", i)))
+        ctx.n, ctx.lane = n, None
+        # avgpool over the whole batch at once: the same reduction as the serial forward
+        return model.fc(torch.cat(feats).mean(dim=(1, 2)))
+    if len(parts) == 1:
         return model.fc(_features(model, x, ctx))
     feats = []
-    for s in range(0, n, c):
+    for s0, s1 in parts:
         if ctx is not None:
-            ctx.n = min(c, n - s)
-        feats.append(_features(model, x[s:s + c], ctx))
+            ctx.n = s1 - s0
+        feats.append(_features(model, x[s0:s1], ctx))
     if ctx is not None:
         ctx.n = n
     return model.fc(torch.cat(feats))
@@ -402,7 +475,8 @@ def _static_eager(model, x, cal):
 
 
 def _graph_key(model, x, cal):
-    return (tuple(x.shape), x.dtype, x.device, cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0])
+    return (tuple(x.shape), x.dtype, x.device, cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0],
+            CONCURRENT_DS[0], STREAMS[0])
 
 
 def _graph_ready(model, x, cal):

@@ -531,7 +531,9 @@ def alg_work(n, h, w, cin, cout, kh, kw, ho, wo, limbs, wlimbs, y_f32, y_q, res_
     macs = n * ho * wo * cout * kh * kw * cin
     out_elems = n * ho * wo * cout
     per_out = (4 if y_f32 else 0) + (limbs if y_q else 0) + (4 if res_f32 else 0) + (limbs if res_q else 0)
-    nbytes = limbs * n * h * w * cin + wlimbs * cout * kh * kw * cin + out_elems * per_out
+    # a strided 1x1 conv reads only the pixels it samples (1/stride^2 of its input)
+    in_elems = n * ho * wo * cin if (kh == 1 and kw == 1) else n * h * w * cin
+    nbytes = limbs * in_elems + wlimbs * cout * kh * kw * cin + out_elems * per_out
     return {"ops": 2 * macs, "bytes": nbytes, "passes": limbs * wlimbs - _skipped_passes(limbs, wlimbs),
             "shape": "%4d->%4d k%d %3d->%3d %s%s" % (cin, cout, kh, h, ho, "f" if y_f32 else "-",
                                                     "r" if (res_f32 or res_q) else "-")}

@@ -794,6 +794,35 @@ def test_fused_stem_in_the_model(gpu):
     assert torch.equal(a, b) and torch.equal(a, c)
 
 
+@pytest.mark.parametrize("arch,assign", [("resnet50", "r50_mixed"), ("resnet18", "r18_u8")])
+def test_concurrent_streams_bitwise(gpu, arch, assign):
+    """The downsample branch on a side stream and the batch split into 2 / 3 slices on their own
+    streams (fork/join, eager and inside the captured graph) give the same logits, bit for bit, as
+    the serial forward."""
+    from smpq import engine
+    net = build_model(gpu, arch, assign)
+    x = torch.randn(7, 3, 224, 224, generator=torch.Generator().manual_seed(23)).to(gpu)
+    x2 = torch.randn(7, 3, 224, 224, generator=torch.Generator().manual_seed(24)).to(gpu)
+    old = engine.CONCURRENT_DS[0], engine.USE_GRAPH[0], engine.STREAMS[0]
+    got = []
+    try:
+        with torch.no_grad():
+            engine.CONCURRENT_DS[0], engine.USE_GRAPH[0], engine.STREAMS[0] = False, False, 1
+            net(x)  # calibrate
+            a, a2 = net(x), net(x2)
+            for streams in (1, 2, 3):
+                engine.STREAMS[0] = streams
+                engine.CONCURRENT_DS[0], engine.USE_GRAPH[0] = True, False
+                got += [(net(x), a), (net(x2), a2)]  # eager, forked
+                engine.USE_GRAPH[0] = True
+                got += [(net(x), a), (net(x2), a2), (net(x), a)]  # capture, replays
+    finally:
+        engine.CONCURRENT_DS[0], engine.USE_GRAPH[0], engine.STREAMS[0] = old
+    torch.cuda.synchronize()
+    for i, (g, want) in enumerate(got):
+        assert torch.equal(g, want), i
+
+
 @pytest.mark.parametrize("limbs", [2, 3])
 def test_maxpool_quantize(gpu, limbs):
     from smpq import ops

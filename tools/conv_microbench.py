@@ -26,6 +26,9 @@ SHAPES = [  # name, cin, cout, k, stride, hin, residual
     ("c3_64_256_56", 64, 256, 1, 1, 56, True),
     ("ds_64_256_56", 64, 256, 1, 1, 56, False),
     ("c2_256_256_14", 256, 256, 3, 1, 14, False),
+    ("c2_128_128_28", 128, 128, 3, 1, 28, False),
+    ("c2_512_512_7", 512, 512, 3, 1, 7, False),
+    ("c1_2048_512_7", 2048, 512, 1, 1, 7, False),
     ("c3_256_1024_14", 256, 1024, 1, 1, 14, True),
     ("c1_1024_256_14", 1024, 256, 1, 1, 14, False),
 ]
