@@ -59,7 +59,7 @@ FUSED_STEM = [_os.environ.get("SMPQ_FUSED_STEM", "1") != "0"]
 # static range: the downsample branch of a block runs on a side stream beside conv1 / conv2
 CONCURRENT_DS = [_os.environ.get("SMPQ_CONCURRENT_DS", "1") != "0"]
 # static range: the batch split into this many slices, each on its own stream (concurrent kernels)
-STREAMS = [int(_os.environ.get("SMPQ_STREAMS", "1"))]
+STREAMS = [int(_os.environ.get("SMPQ_STREAMS", "2"))]
 stats.setdefault("graph_captures", 0)
 stats.setdefault("graph_replays", 0)
 
