@@ -27,6 +27,8 @@
  *   smpq_softmax_xent              per-batch body of functions.py:84-129 evaluate_acc_loss_softmax
  *                                  (output.max(1), CrossEntropyLoss, Softmax(dim=1), :113-121)
  *   smpq_kl_rows                   functions.py:131-149 KLdiv (per-image sum_c n*log(n/o), :140-146)
+ *   smpq_bottleneck_tail_q         Bottleneck.forward's conv2 -> bn2 -> relu -> conv3 -> bn3 -> += identity
+ *                                  -> relu (resnet.py:103-114) as one launch
  */
 #ifndef SMPQ_H_
 #define SMPQ_H_
@@ -226,6 +228,28 @@ int smpq_stem_pool_supported(int n, int h, int w, int cout, int limbs, int wlimb
 int smpq_stem_pool_s2d_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, const int8_t* codes,
                          int wlimbs, int cout, const float* col_scale, const float* col_shift, int limbs,
                          int8_t* yq, float yq_range, int32_t* overflow, smpq_stream_t stream);
+
+/* Fused Bottleneck tail, static-range mode (Bottleneck.forward resnet.py:103-114: conv2 + bn2 +
+ * relu, conv3 + bn3, out += identity, relu) in ONE launch: the conv2 output t2 stays in LDS.
+ * Inputs: t1's limb planes xq [limbs][n][h][w][cmid] with per-image range x_absmax (as
+ * smpq_conv2d_fwd_q), conv2 codes2 [cmid][kh*kw*cmid] (one limb, + offset2 or NULL), its folded
+ * column scale / shift, relu2, and t2's static range range2; conv3 codes3 [cout3][cmid] (one limb,
+ * + offset3 or NULL), folded scale / shift, the residual's limb planes residual_q
+ * [limbs][n][ho][wo][cout3] with residual_range, relu3; output yq [limbs][n][ho][wo][cout3] with
+ * range yq_range; *overflow set to 1 when t2 or the output exceeded its range. Bitwise identical to
+ * smpq_conv2d_fwd_q(conv2 -> t2 planes with range2) followed by smpq_conv2d_fwd_q(conv3 with the
+ * residual planes). Requires cout3 == 4 * cmid, cmid % 64 == 0, limbs 2 or 3, and a tile config
+ * for which smpq_bottleneck_tail_supported(cfg, cmid, cout3, kh, kw, limbs) == 1 (its block covers
+ * all cmid channels of its pixels). */
+int smpq_bottleneck_tail_num_configs(void);
+int smpq_bottleneck_tail_supported(int cfg, int cmid, int cout3, int kh, int kw, int limbs);
+int smpq_bottleneck_tail_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cmid,
+                           const int8_t* codes2, const int32_t* offset2, int kh, int kw, int stride, int pad,
+                           const float* col_scale2, const float* col_shift2, int relu2, float range2,
+                           const int8_t* codes3, const int32_t* offset3, int cout3, const float* col_scale3,
+                           const float* col_shift3, const int8_t* residual_q, float residual_range, int relu3,
+                           int limbs, int8_t* yq, float yq_range, int32_t* overflow, int tile_cfg,
+                           smpq_stream_t stream);
 
 /* Tile configurations of smpq_conv2d_fwd (for autotuning): count, and BM (pixels) x BN (output
  * channels) / threads. Every configuration gives bitwise-identical results. */

@@ -58,6 +58,11 @@ _PROTOS = {
                                   ctypes.c_float, _vp, _i, _vp]),
     "smpq_stem_pool_supported": (_i, [_i] * 6),
     "smpq_stem_pool_s2d_q": (_i, [_vp, _vp, _i, _i, _i, _vp, _i, _i, _vp, _vp, _i, _vp, ctypes.c_float, _vp, _vp]),
+    "smpq_bottleneck_tail_num_configs": (_i, []),
+    "smpq_bottleneck_tail_supported": (_i, [_i] * 6),
+    "smpq_bottleneck_tail_q": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i,
+                                    ctypes.c_float, _vp, _vp, _i, _vp, _vp, _vp, ctypes.c_float, _i, _i, _vp,
+                                    ctypes.c_float, _vp, _i, _vp]),
     "smpq_conv2d_num_tile_configs": (_i, []),
     "smpq_conv2d_tile_config": (_i, [_i, _vp, _vp, _vp]),
     "smpq_conv2d_tile_kind": (_i, [_i]),

@@ -273,15 +273,59 @@ def block_forward(blk, x, ctx=None, last=False):
 
     if hasattr(blk, "conv3"):  # Bottleneck (resnet.py:97-116)
         t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
-        t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
-        join()
-        return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax,
-                        want_f32=last)
+
+        def tail():
+            t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
+            join()
+            return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax,
+                            want_f32=last)
+        if not last:
+            fused = _fused_tail(blk, t1, identity, ctx, join, tail)
+            if fused is not None:
+                return fused
+        return tail()
     # BasicBlock (resnet.py:55-68)
     t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
     join()
     return run_conv(blk.conv2, blk.bn2, t1, True, residual=identity, ctx=ctx, want_amax=out_amax,
                     want_f32=last)
+
+
+def _fused_tail(blk, t1, identity, ctx, join, unfused):
+    """Static mode: conv2 + bn2 + relu + conv3 + bn3 + identity + relu of a Bottleneck
+    (resnet.py:103-114) as one launch (ops.bottleneck_tail_q: t2 stays on chip) when both convs
+    carry exact int8 codes and the autotuner finds it faster than the two launches; returns the
+    block output Act, or None for the two-launch path."""
+    if ctx is None or ctx.ranges is None or not isinstance(identity, Act) or identity.q is None \
+            or identity.f32 is not None or identity.rng is None or t1.q is None or t1.rng is None:
+        return None
+    c2, c3 = blk.conv2, blk.conv3
+    if id(c2) not in ctx.ranges or id(c3) not in ctx.ranges or c2.kernel_size[0] != c2.kernel_size[1] \
+            or c3.kernel_size != (1, 1) or c3.stride != (1, 1) or c3.padding != (0, 0):
+        return None
+    p2, p3 = conv_plan(c2, blk.bn2), conv_plan(c3, blk.bn3)
+    if p2 is None or p3 is None or p2[4] != "exact8" or p3[4] != "exact8":
+        return None
+    limbs, cmid = t1.q.shape[0], t1.q.shape[-1]
+    if c2.out_channels != cmid or c3.in_channels != cmid or c3.out_channels != 4 * cmid:
+        return None
+    box = []
+
+    def two_launches():
+        a = unfused()
+        box.append(a)
+        return a.q
+    join()  # the fused launch reads the identity (downsample branch) from its first chunk on
+    rng3 = ctx.ranges[id(c3)]
+    h0 = stats["hip_conv"]  # the autotuner may run the two-launch path several times: count 2 convs
+    yq = ops.tuned_bottleneck_tail(
+        two_launches, t1.q, t1.amax, p2[0], p2[1], c2.kernel_size[0], c2.stride[0], c2.padding[0], p2[2], p2[3],
+        ctx.ranges[id(c2)], p3[0], p3[1], p3[2], p3[3], identity.q, identity.rng, rng3, ctx.overflow)
+    stats["hip_conv"] = h0 + 2
+    if box and box[-1].q is yq:
+        return box[-1]
+    c2.last_path = c3.last_path = "hip-exact8-tail"
+    return Act(q=yq, amax=ctx.range_tensor(c3), rng=rng3)
 
 
 def stem_s2d_plan(conv, bn):

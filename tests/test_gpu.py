@@ -1090,3 +1090,111 @@ def test_device_fingerprint_matches_host(gpu):
     fp.tensors[1][12345] += 1.0
     fp.check(flag)
     assert int(flag.item()) == 1
+
+
+def _tail_case(gpu, n, h, cmid, stride, limbs, seed, offsets=True):
+    """Random conv2 (3x3) / conv3 (1x1, 4 cmid) weights with 8-bit off-centre channels (offsets),
+    t1 limb planes, the residual's limb planes."""
+    from smpq import ops
+    g = torch.Generator(device=gpu).manual_seed(seed)
+    cout3 = 4 * cmid
+
+    def weights(cout, cin, k):
+        w = torch.randn(cout, cin, k, k, device=gpu, generator=g) * 0.05
+        bits = [6] * cout
+        if offsets:
+            for c in range(0, cout, 3):
+                w[c] = w[c].abs() + 0.02  # all-positive channel: 8-bit codes off-centre
+                bits[c] = 8
+        step = ops.quantize_channels_(w.reshape(cout, -1), bits)
+        codes, off, wscale, st = ops.pack_weights_ex(w, step, 1)
+        assert int(st.cpu()[0]) == 0 and int(st.cpu()[1]) == 0
+        cs = (wscale * (0.5 + torch.rand(cout, device=gpu, generator=g))).contiguous()
+        sh = (0.1 * torch.randn(cout, device=gpu, generator=g)).contiguous()
+        return codes, (off if bool((off != 0).any()) else None), cs, sh
+
+    c2 = weights(cmid, cmid, 3)
+    c3 = weights(cout3, cmid, 1)
+    assert not offsets or (c2[1] is not None and c3[1] is not None)
+    r1 = 3.0
+    x = torch.relu(torch.randn(n, h, h, cmid, device=gpu, generator=g))
+    am = torch.full((n,), r1, device=gpu)
+    xq = ops.act_quantize(x, am, limbs)
+    ho = (h + 2 - 3) // stride + 1
+    rr = 4.0
+    res = torch.relu(torch.randn(n, ho, ho, cout3, device=gpu, generator=g))
+    resq = ops.act_quantize(res, torch.full((n,), rr, device=gpu), limbs)
+    return xq, am, c2, c3, resq, rr, ho
+
+
+def _glds_cfg(cin, cout, k, limbs):
+    """An LDS-DMA tile config for this conv (the family the engine runs: its static epilogue is
+    the lean one the fused tail shares; the register-staged family rounds the general way)."""
+    from smpq import ops
+    return next(c for c in ops.tile_configs() if ops.tile_kind(c) in (ops.TILE_LDS_DMA, ops.TILE_LDS_DMA_K128)
+                and ops._tile_fits(c, limbs, 1, False, cout, cin, k))
+
+
+def _tail_two_launches(xq, am, c2, c3, stride, r2, resq, rr, r3):
+    from smpq import ops
+    limbs, n, cmid = xq.shape[0], xq.shape[1], xq.shape[-1]
+    ovf = torch.zeros(2, dtype=torch.int32, device=xq.device)
+    _, t2 = ops.conv2d_q(xq, am, c2[0], c2[1], 3, 3, stride, 1, c2[2], c2[3], relu=True, emit_range=r2,
+                         overflow=ovf, want_f32=False, tile_cfg=_glds_cfg(cmid, cmid, 3, limbs))
+    _, y = ops.conv2d_q(t2, torch.full((n,), r2, device=xq.device), c3[0], c3[1], 1, 1, 1, 0, c3[2], c3[3],
+                        relu=True, emit_range=r3, overflow=ovf, want_f32=False, residual_q=resq, residual_range=rr,
+                        tile_cfg=_glds_cfg(cmid, 4 * cmid, 1, limbs))
+    return y, int(ovf[0].item())
+
+
+@pytest.mark.parametrize("limbs", [2, 3])
+@pytest.mark.parametrize("n,h,cmid,stride", [(3, 20, 64, 1), (2, 17, 128, 2), (3, 9, 256, 1), (2, 7, 512, 1),
+                                              (2, 14, 512, 2)])
+def test_bottleneck_tail_bitwise(gpu, limbs, n, h, cmid, stride):
+    """The fused tail (conv2 + bn2 + relu + conv3 + bn3 + residual + relu, t2 kept in LDS) gives the
+    two-launch path's output limb planes and overflow flag bit for bit, for every tile config that
+    takes the shape: partial pixel tiles, stride 2, weight offsets on both convs, and ranges that
+    overflow in t2 or in the output."""
+    from smpq import ops
+    xq, am, c2, c3, resq, rr, ho = _tail_case(gpu, n, h, cmid, stride, limbs, 40 + cmid + h)
+    cfgs = [c for c in ops.tail_configs() if ops.tail_supported(c, cmid, 4 * cmid, 3, limbs)]
+    assert cfgs
+    for r2, r3, want in ((40.0, 60.0, None), (0.05, 60.0, 1), (40.0, 0.05, 1)):
+        ref, ovf_ref = _tail_two_launches(xq, am, c2, c3, stride, r2, resq, rr, r3)
+        if want is not None:
+            assert ovf_ref == want
+        for cfg in cfgs:
+            ovf = torch.zeros(2, dtype=torch.int32, device=gpu)
+            got = ops.bottleneck_tail_q(xq, am, c2[0], c2[1], 3, stride, 1, c2[2], c2[3], r2, c3[0], c3[1], c3[2],
+                                        c3[3], resq, rr, r3, ovf, cfg)
+            assert got.shape == ref.shape == (limbs, n, ho, ho, 4 * cmid)
+            assert torch.equal(got, ref), (cfg, r2, r3, (got != ref).sum().item())
+            assert int(ovf[0].item()) == ovf_ref, (cfg, r2, r3)
+
+
+def test_bottleneck_tail_in_the_model(gpu):
+    """R50 static-range forward with every eligible Bottleneck tail fused (forced, each tile
+    config family) == the two-launch forward, bit for bit (eager and graph replay)."""
+    from smpq import engine, ops
+    net = build_model(gpu, "resnet50", "r50_mixed")
+    x = torch.randn(6, 3, 224, 224, generator=torch.Generator().manual_seed(25)).to(gpu)
+    old = ops.TAIL_FUSION[0], ops.TAIL_FORCE[0], engine.USE_GRAPH[0]
+    outs = []
+    try:
+        with torch.no_grad():
+            ops.TAIL_FUSION[0], engine.USE_GRAPH[0] = False, False
+            net(x)  # calibrate
+            ref = net(x)
+            ops.TAIL_FUSION[0] = True
+            for force in (0, 1, 3, 5, 8):
+                ops.TAIL_FORCE[0] = force
+                outs.append(net(x))
+                assert net.layer1[1].conv2.last_path == "hip-exact8-tail"
+            ops.TAIL_FORCE[0] = None
+            ops._TUNED_TAIL.clear()
+            engine.USE_GRAPH[0] = True
+            outs += [net(x), net(x), net(x)]  # autotuned, capture, replay
+    finally:
+        ops.TAIL_FUSION[0], ops.TAIL_FORCE[0], engine.USE_GRAPH[0] = old
+    for i, y in enumerate(outs):
+        assert torch.equal(y, ref), i
