@@ -233,6 +233,8 @@ def main():
     if rank == 0:
         print("autotuned tiles:", {"x".join(map(str, k[:8])): v for k, v in ops._TUNED.items()},
               file=sys.stderr, flush=True)
+        print("fused bottleneck tails (-1 = two launches):",
+              {"x".join(map(str, k)): v for k, v in ops._TUNED_TAIL.items()}, file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarize a rocprofv3 --kernel-trace --stats run of bench.py: per-kernel totals and the
 average duration of the quantized-conv launches (to check bench.py's event-timed avg_launch_ms).
-usage: python tools/rocprof_summary.py <run_kernel_stats.csv> [run_kernel_trace.csv]"""
+usage: python tools/rocprof_summary.py <run_kernel_stats.csv> [run_kernel_trace.csv [L steps rsteps]]"""
 import csv
 import sys
 
@@ -27,8 +27,5 @@ if len(sys.argv) > 2:
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in tr]
     roof = dur[-rsteps * L:]
-    timed = dur[-(rsteps + 1 + steps) * L:-(rsteps + 1) * L]
-    print("roofline region (last %d launches, eager): avg %.5f ms/launch, %.3f ms/step"
+    print("roofline region (last %d launches, eager, one launch at a time): avg %.5f ms/launch, %.3f ms/step"
           % (len(roof), sum(roof) / len(roof), sum(roof) / rsteps))
-    print("timed region (%d launches, graph replay): avg %.5f ms/launch, %.3f ms/step"
-          % (len(timed), sum(timed) / len(timed), sum(timed) / steps))
