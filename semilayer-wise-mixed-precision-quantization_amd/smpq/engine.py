@@ -422,12 +422,14 @@ def _forward(model, x, ctx):
     c = CHUNK[0]
     parts = [(s, min(n, s + c)) for s in range(0, n, c)]
     nst = STREAMS[0] if (ctx is not None and ctx.ranges is not None) else 1
-    if nst > 1 and len(parts) == 1 and n >= 2 * nst:
+    if nst > 1 and n >= 2 * nst:
         # static mode: the batch as nst concurrent slices, each on its own stream, so that one
         # slice's bandwidth-bound convs overlap another's MFMA/L2-bound ones; every image's result
-        # is the same as in the serial forward (per-layer ranges are fixed, kernels exact)
-        step = (n + nst - 1) // nst
-        parts = [(s, min(n, s + step)) for s in range(0, n, step)]
+        # is the same as in the serial forward (per-layer ranges are fixed, kernels exact). With
+        # chunking (CHUNK < n) the chunks go round-robin over the nst streams instead.
+        if len(parts) == 1:
+            step = (n + nst - 1) // nst
+            parts = [(s, min(n, s + step)) for s in range(0, n, step)]
         main = torch.cuda.current_stream()
         for s0, s1 in parts:  # shared per-layer range tensors exist before the fork
             ctx.n = s1 - s0
@@ -435,13 +437,14 @@ def _forward(model, x, ctx):
                 if id(m) in ctx.ranges:
                     ctx.range_tensor(m)
         feats = []
+        lanes = min(nst, len(parts))
+        for i in range(lanes):
+            _stream((x.device, "slice", i)).wait_stream(main)
         for i, (s0, s1) in enumerate(parts):
-            st = _stream((x.device, "slice", i))
-            st.wait_stream(main)
-            with torch.cuda.stream(st):
-                ctx.n, ctx.lane = s1 - s0, i
+            with torch.cuda.stream(_stream((x.device, "slice", i % lanes))):
+                ctx.n, ctx.lane = s1 - s0, i % lanes
                 feats.append(_features(model, x[s0:s1], ctx, pool=False))
-        for i in range(len(parts)):
+        for i in range(lanes):
             main.wait_stream(_stream((x.device, "slice", i)))
         ctx.n, ctx.lane = n, None
         # avgpool over the whole batch at once: the same reduction as the serial forward

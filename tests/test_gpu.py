@@ -864,23 +864,31 @@ def test_static_ranges_overflow_falls_back_to_dynamic(gpu):
 
 @pytest.mark.parametrize("mode", ["dynamic", "static"])
 def test_chunked_forward_identical(gpu, mode):
-    """Infinity-Cache batch chunking changes no result (per-image independence)."""
+    """Infinity-Cache batch chunking changes no result (per-image independence), also with the
+    chunks round-robin over 1 / 2 / 3 concurrent streams (static mode; eager and graph replay)."""
     from smpq import engine
     net = build_model(gpu, "resnet50", "r50_mixed")
     x = torch.randn(12, 3, 224, 224, generator=torch.Generator().manual_seed(13)).to(gpu)
     engine.set_range_mode(mode)
-    old = engine.CHUNK[0]
+    old = engine.CHUNK[0], engine.STREAMS[0], engine.USE_GRAPH[0]
+    got = []
     try:
         with torch.no_grad():
             engine.set_chunk(64)
             net(x)  # calibrates in static mode
             a = net(x)
             engine.set_chunk(5)
-            b = net(x)
+            for streams in (1, 2, 3):
+                engine.STREAMS[0] = streams
+                for graph in (False, True):
+                    engine.USE_GRAPH[0] = graph
+                    got += [net(x), net(x)]
     finally:
-        engine.set_chunk(old)
+        engine.set_chunk(old[0])
+        engine.STREAMS[0], engine.USE_GRAPH[0] = old[1], old[2]
         engine.set_range_mode("static")
-    assert torch.equal(a, b)
+    for i, b in enumerate(got):
+        assert torch.equal(a, b), i
 
 
 def test_graph_replay_matches_eager(gpu):
