@@ -1206,3 +1206,31 @@ def test_bottleneck_tail_in_the_model(gpu):
         ops.TAIL_FUSION[0], ops.TAIL_FORCE[0], engine.USE_GRAPH[0] = old
     for i, y in enumerate(outs):
         assert torch.equal(y, ref), i
+
+
+def test_bench_workload_parity_full_size(gpu):
+    """Parity at BASELINE.json configs[2]'s full size: the bench's workload (R50 mixed 8/6/4,
+    B=256, L=3, static ranges, HIP graph, two stream slices) on the BN-recalibrated parity model
+    vs the reference's CPU forward restated in oracle/torch_ref.py (the same torch-CPU operators)
+    on the same fake-quantized weights and the same 256 images. Stated tolerance:
+    max |logit - ref| <= 2e-4 max |ref|; top-1 identical wherever the reference's top-1 margin
+    exceeds twice that error (near-ties may legitimately flip under any fp32 reordering)."""
+    from oracle import torch_ref
+    from smpq import engine, ops
+    assert ops.get_act_limbs() == 3 and engine.get_range_mode() == "static"
+    net = build_model(gpu, "resnet50", "r50_mixed", "r50_mixed_cal")
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items() if not k.endswith(("qbits", "qstep"))}
+    x = torch.randn(256, 3, 224, 224, generator=torch.Generator().manual_seed(2024))
+    with torch.no_grad():
+        net(x.to(gpu))  # calibration
+        y = net(x.to(gpu))  # graph capture
+        y = net(x.to(gpu)).double().cpu()  # graph replay: the bench's timed path
+    ref = torch_ref.resnet_forward("resnet50", sd, x).double()
+    err = ((y - ref).abs().max() / ref.abs().max()).item()
+    assert err <= 2e-4, err
+    top2 = ref.topk(2, dim=1).values
+    sure = (top2[:, 0] - top2[:, 1]) > 2 * err * ref.abs().max()
+    print("full-size parity: max rel logit err %.2e, top-1 decided on %d/256, all equal: %s"
+          % (err, sure.sum().item(), torch.equal(y.argmax(1), ref.argmax(1))))
+    assert sure.sum().item() >= 128, sure.sum().item()  # most images are decided
+    assert torch.equal(y.argmax(1)[sure], ref.argmax(1)[sure])
