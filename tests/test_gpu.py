@@ -410,6 +410,7 @@ def test_model_logits_vs_reference(gpu, case, arch, assign, batch, limbs, mode):
             w = net.state_dict()[k[len(case + "/qsum/"):]].double().cpu()
             np.testing.assert_allclose([w.sum().item(), w.abs().sum().item()], g[k], rtol=1e-12, atol=1e-12)
     x = torch.randn(batch, 3, 224, 224, generator=torch.Generator().manual_seed(1))
+    old_limbs = ops.get_act_limbs()
     ops.set_act_limbs(limbs)
     engine.set_range_mode(mode)
     engine.USE_GRAPH[0] = False  # count launches of one eager forward (graphs: test_graph_replay_*)
@@ -428,7 +429,7 @@ def test_model_logits_vs_reference(gpu, case, arch, assign, batch, limbs, mode):
         slices = engine.STREAMS[0] if (mode == "static" and xg.shape[0] >= 2 * engine.STREAMS[0]) else 1
         assert stats["hip_conv"] - before == nq * slices  # every conv incl. stem + downsample on HIP
     finally:
-        ops.set_act_limbs(2)
+        ops.set_act_limbs(old_limbs)
         engine.set_range_mode("static")
         engine.USE_GRAPH[0] = True
     ref = g[case + "/logits"].astype(np.float64)
@@ -1217,14 +1218,20 @@ def test_bench_workload_parity_full_size(gpu):
     exceeds twice that error (near-ties may legitimately flip under any fp32 reordering)."""
     from oracle import torch_ref
     from smpq import engine, ops
-    assert ops.get_act_limbs() == 3 and engine.get_range_mode() == "static"
-    net = build_model(gpu, "resnet50", "r50_mixed", "r50_mixed_cal")
-    sd = {k: v.detach().cpu() for k, v in net.state_dict().items() if not k.endswith(("qbits", "qstep"))}
-    x = torch.randn(256, 3, 224, 224, generator=torch.Generator().manual_seed(2024))
-    with torch.no_grad():
-        net(x.to(gpu))  # calibration
-        y = net(x.to(gpu))  # graph capture
-        y = net(x.to(gpu)).double().cpu()  # graph replay: the bench's timed path
+    old = ops.get_act_limbs(), engine.get_range_mode()
+    ops.set_act_limbs(3)  # the bench's parity mode
+    engine.set_range_mode("static")
+    try:
+        net = build_model(gpu, "resnet50", "r50_mixed", "r50_mixed_cal")
+        sd = {k: v.detach().cpu() for k, v in net.state_dict().items() if not k.endswith(("qbits", "qstep"))}
+        x = torch.randn(256, 3, 224, 224, generator=torch.Generator().manual_seed(2024))
+        with torch.no_grad():
+            net(x.to(gpu))  # calibration
+            y = net(x.to(gpu))  # graph capture
+            y = net(x.to(gpu)).double().cpu()  # graph replay: the bench's timed path
+    finally:
+        ops.set_act_limbs(old[0])
+        engine.set_range_mode(old[1])
     ref = torch_ref.resnet_forward("resnet50", sd, x).double()
     err = ((y - ref).abs().max() / ref.abs().max()).item()
     assert err <= 2e-4, err
