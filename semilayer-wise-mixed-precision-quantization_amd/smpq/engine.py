@@ -3,16 +3,23 @@
 Restates ``ResNet._forward_impl`` (resnet.py:204-220), ``BasicBlock.forward`` (resnet.py:55-68)
 and ``Bottleneck.forward`` (resnet.py:97-116):
 
-  * input: per-image range + quantization of the NCHW image into 4-channel NHWC limb planes
-    (``image_quantize``);
-  * stem conv 7x7/2 + BN + ReLU (resnet.py:143-146) = one ``conv2d_q`` launch (fp32 weights as
-    2 int8 limbs), then MaxPool 3x3/2 fused with the quantization of its output
-    (``maxpool_quantize``);
-  * every block conv + its BN (+ residual add) (+ ReLU) = one ``conv2d_q`` launch whose
-    epilogue also yields the per-image max|y| the NEXT conv's activation quantizer needs;
+  * input: per-image range + quantization of the NCHW image into space-to-depth limb planes
+    (``image_quantize_s2d``; 16-channel pixels = 2x2 blocks of RGB + 0);
+  * stem conv 7x7/2 + BN + ReLU + MaxPool 3x3/2 (resnet.py:143-147): static mode, ONE launch
+    (``stem_pool_s2d``: only the pooled limb planes leave the CU); dynamic mode, the stem conv
+    (fp32 weights as 24-bit fixed point) then the pool fused with its output's quantization;
+  * every block conv + its BN (+ residual add) (+ ReLU) = one ``conv2d_q`` launch; static mode:
+    its epilogue writes the NEXT conv's limb planes, dynamic mode: fp32 + the per-image max|y| the
+    next conv's quantizer needs; optionally conv2 + conv3 of a Bottleneck as one launch
+    (``bottleneck_tail_q``, kept only where the autotuner finds it faster);
   * the downsample 1x1 conv + BN (resnet.py:188-192) reads the block input's limb planes
-    (already quantized for conv1) and writes the fp32 identity consumed by conv3's epilogue;
+    (already quantized for conv1) and writes the identity (static mode: as limb planes) consumed
+    by conv3's epilogue;
   * avgpool + fc (resnet.py:216-218) stay torch ops (2 MMAC/image).
+
+Static mode runs the batch as ``STREAMS`` slices on their own streams (or, unsliced, each
+downsample branch on a side stream), fork/join inside the captured HIP graph; every launch computes
+what it computes serially, so the logits are bitwise those of the serial forward.
 
 An activation is carried as ``Act`` = fp32 NHWC tensor and/or its int8 limb planes plus its
 per-image range; limb planes are produced at most once per activation.
