@@ -3,10 +3,19 @@
 (BASELINE.json metric; configs[2] at N=1: batch 256 on one MI355X; configs[3] at N=8:
 batch 2048 = 8 x 256, weak scaling, RCCL all-gather of logits).
 
-python bench.py --gpus N --steps K --warmup W       (N > 1: launched by torch.distributed.run)
+python bench.py --gpus N --steps K --warmup W
 
-One step = one fused forward of 256 synthetic 224x224 images per GPU (inputs generated on
-device, resident in HBM before the timed region) + the all-gather of the logits. Prints ONE
+N > 1: one process per GPU. Under torch.distributed.run (WORLD_SIZE set) this process is one
+rank; started directly with --gpus N it launches `python -m torch.distributed.run
+--nproc-per-node N` on itself as a child process before touching the GPU and exits with its code.
+
+One step = one fused forward of 256 synthetic 224x224 images per GPU + the all-gather of the
+logits. The inputs are --batches distinct global batches (each rank holds its shard of every
+one, generated on device and resident in HBM before the timed region); the first warm-up step
+calibrates the static ranges on batch 0, as a real evaluation calibrates on its first batch, and
+the timed steps cycle through all of them. Ranks calibrate together (engine.set_dp_group: the
+per-layer maxima are MAX-all-reduced), so the gathered logits equal a single-GPU forward of the
+global batch bit for bit. Prints ONE
 JSON line on rank 0 with the roofline of the dominant kernel family (the quantized conv:
 qconv_glds_kernel / qconv_kernel, every launch incl. the stem) and the CPU baseline (the
 reference's fp32 torch-CPU forward restated in oracle/torch_ref.py, timed on a bounded sample).
@@ -187,11 +196,27 @@ def main():
     ap.add_argument("--chunk", type=int, default=None, help="images per pass (Infinity-Cache blocking)")
     ap.add_argument("--streams", type=int, default=None,
                     help="batch slices run concurrently on their own streams (default: engine.STREAMS)")
+    ap.add_argument("--batches", type=int, default=4,
+                    help="distinct device-resident global batches cycled through the timed steps")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: relaunch under torch.distributed.run as a CHILD (no exec), before
+        # this process touches the GPU
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
@@ -213,37 +238,45 @@ def main():
         engine.set_chunk(args.chunk)
     if args.streams:
         engine.STREAMS[0] = args.streams
+    if world > 1:
+        engine.set_dp_group(dist.group.WORLD)  # ranks calibrate together (MAX-all-reduced maxima)
     torch.manual_seed(0)
     net = getattr(resnet, arch)().to(dev).eval()
     assignments.apply_assignment(net, assign)
 
-    # this rank's shard of the global batch (dp.shard_range), generated on device
+    # this rank's shard of every global batch (dp.shard_range), generated on device; the seed
+    # depends on the batch and the shard's first image only
     s0, s1 = dp.shard_range(args.batch * world, rank, world)
-    g = torch.Generator(device=dev).manual_seed(1000 + s0)
-    x = torch.randn(s1 - s0, 3, 224, 224, generator=g, device=dev)
+    xs = []
+    for b in range(max(1, args.batches)):
+        g = torch.Generator(device=dev).manual_seed(1000 + 1000003 * b + s0)
+        xs.append(torch.randn(s1 - s0, 3, 224, 224, generator=g, device=dev))
     gathered = torch.empty(world * args.batch, 1000, device=dev) if world > 1 else None
+    it = [0]
 
     def step():
+        x = xs[it[0] % len(xs)]
+        it[0] += 1
         with torch.no_grad():
             y = net(x)
             return dp.gather_logits(y, world, out=gathered)
 
-    for _ in range(args.warmup):
-        step()
+    for _ in range(max(1, args.warmup)):
+        step()  # the first one calibrates on batch 0
     if rank == 0:
         print("autotuned tiles:", {"x".join(map(str, k[:8])): v for k, v in ops._TUNED.items()},
               file=sys.stderr, flush=True)
-        print("fused bottleneck tails (-1 = two launches):",
-              {"x".join(map(str, k)): v for k, v in ops._TUNED_TAIL.items()}, file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    st0 = {k: stats[k] for k in ("calibrations", "overflow_reruns", "stale_reruns", "graph_captures")}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    timed_stats = {k: stats[k] - v for k, v in st0.items()}
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
@@ -296,7 +329,13 @@ def main():
                        "range_mode": engine.get_range_mode(), "chunk": engine.CHUNK[0],
                        "hip_graph": bool(engine.USE_GRAPH[0]),
                        "concurrent_downsample": bool(engine.CONCURRENT_DS[0]),
-                       "batch_slices_on_streams": engine.STREAMS[0]},
+                       "batch_slices_on_streams": engine.STREAMS[0],
+                       "distinct_batches": len(xs),
+                       "calibrations_total": stats["calibrations"],
+                       "timed_calibrations": timed_stats["calibrations"],
+                       "timed_overflow_reruns": timed_stats["overflow_reruns"],
+                       "timed_stale_reruns": timed_stats["stale_reruns"],
+                       "timed_graph_captures": timed_stats["graph_captures"]},
             "roofline": roof,
         }
         if not args.no_cpu_baseline and world == 1:

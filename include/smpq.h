@@ -27,8 +27,8 @@
  *   smpq_softmax_xent              per-batch body of functions.py:84-129 evaluate_acc_loss_softmax
  *                                  (output.max(1), CrossEntropyLoss, Softmax(dim=1), :113-121)
  *   smpq_kl_rows                   functions.py:131-149 KLdiv (per-image sum_c n*log(n/o), :140-146)
- *   smpq_bottleneck_tail_q         Bottleneck.forward's conv2 -> bn2 -> relu -> conv3 -> bn3 -> += identity
- *                                  -> relu (resnet.py:103-114) as one launch
+ *   smpq_avgpool_fc                avgpool + flatten + fc of ResNet._forward_impl (resnet.py:216-218),
+ *                                  batch-invariant (sharded logits == single-GPU logits, bitwise)
  */
 #ifndef SMPQ_H_
 #define SMPQ_H_
@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SMPQ_ABI_VERSION 1
+#define SMPQ_ABI_VERSION 2
 
 /* status codes */
 #define SMPQ_OK 0
@@ -56,6 +56,9 @@ typedef void* smpq_stream_t; /* hipStream_t */
 
 int smpq_abi_version(void);
 const char* smpq_last_error(void);
+/* SHA-256 (hex) of the sources, headers and compiler flags this library was built from;
+ * __graft_entry__.build() rebuilds whenever the tree's hash differs from it. */
+const char* smpq_build_stamp(void);
 
 /* Rounding semantics of functions.py:41 `t / scale` (scale a Python float), which depend on
  * where the reference's tensor lives:
@@ -152,7 +155,9 @@ int smpq_maxpool_quantize(const float* x, int n, int h, int w, int c, const floa
  *   limbs      activation code width in int8 limbs: 1 (int8), 2 (int16), 3 (int24)
  *   y          device fp32 NHWC [n][ho][wo][cout]
  *   y_absmax   device fp32 [n] (caller-zeroed), receives max|y| per image, or NULL
- *   tile_cfg   block tile configuration (smpq_conv2d_tile_config), or -1 for the built-in choice */
+ *   tile_cfg   block tile configuration (smpq_conv2d_tile_config), or -1 for the built-in choice:
+ *              an SMPQ_TILE_LDS_DMA(_K128) configuration whenever one takes the shape; the
+ *              register-staged family only for cin == 4 or planes of 2 GiB and more */
 int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                     const int8_t* codes, const int32_t* offset, int cout, int kh, int kw,
                     int stride, int pad, const float* col_scale, const float* col_shift,
@@ -229,27 +234,15 @@ int smpq_stem_pool_s2d_q(const int8_t* xq, const float* x_absmax, int n, int h, 
                          int wlimbs, int cout, const float* col_scale, const float* col_shift, int limbs,
                          int8_t* yq, float yq_range, int32_t* overflow, smpq_stream_t stream);
 
-/* Fused Bottleneck tail, static-range mode (Bottleneck.forward resnet.py:103-114: conv2 + bn2 +
- * relu, conv3 + bn3, out += identity, relu) in ONE launch: the conv2 output t2 stays in LDS.
- * Inputs: t1's limb planes xq [limbs][n][h][w][cmid] with per-image range x_absmax (as
- * smpq_conv2d_fwd_q), conv2 codes2 [cmid][kh*kw*cmid] (one limb, + offset2 or NULL), its folded
- * column scale / shift, relu2, and t2's static range range2; conv3 codes3 [cout3][cmid] (one limb,
- * + offset3 or NULL), folded scale / shift, the residual's limb planes residual_q
- * [limbs][n][ho][wo][cout3] with residual_range, relu3; output yq [limbs][n][ho][wo][cout3] with
- * range yq_range; *overflow set to 1 when t2 or the output exceeded its range. Bitwise identical to
- * smpq_conv2d_fwd_q(conv2 -> t2 planes with range2) followed by smpq_conv2d_fwd_q(conv3 with the
- * residual planes). Requires cout3 == 4 * cmid, cmid % 64 == 0, limbs 2 or 3, and a tile config
- * for which smpq_bottleneck_tail_supported(cfg, cmid, cout3, kh, kw, limbs) == 1 (its block covers
- * all cmid channels of its pixels). */
-int smpq_bottleneck_tail_num_configs(void);
-int smpq_bottleneck_tail_supported(int cfg, int cmid, int cout3, int kh, int kw, int limbs);
-int smpq_bottleneck_tail_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cmid,
-                           const int8_t* codes2, const int32_t* offset2, int kh, int kw, int stride, int pad,
-                           const float* col_scale2, const float* col_shift2, int relu2, float range2,
-                           const int8_t* codes3, const int32_t* offset3, int cout3, const float* col_scale3,
-                           const float* col_shift3, const int8_t* residual_q, float residual_range, int relu3,
-                           int limbs, int8_t* yq, float yq_range, int32_t* overflow, int tile_cfg,
-                           smpq_stream_t stream);
+/* AdaptiveAvgPool2d(1) + flatten + fc (ResNet._forward_impl resnet.py:216-218; modules built at
+ * resnet.py:162-163) on the last block's NHWC fp32 output x [n][hw][c]: pooled[n][c] = (sum over
+ * the hw pixels in order) * (1 / hw), logits[n][nout] = pooled . fc_w[nout][c] (+ fc_b[nout]),
+ * summed over c in order with fused multiply-adds. Every logit is computed in an order that does
+ * not depend on n or on the other images, so an image's logits are the same bits whatever batch
+ * or data-parallel shard it runs in. pooled_ws: device fp32 [n][c] (workspace, holds the pooled
+ * features afterwards); fc_b may be NULL; c % 4 == 0. */
+int smpq_avgpool_fc(const float* x, int n, int hw, int c, const float* fc_w, const float* fc_b, int nout,
+                    float* pooled_ws, float* logits, smpq_stream_t stream);
 
 /* Tile configurations of smpq_conv2d_fwd (for autotuning): count, and BM (pixels) x BN (output
  * channels) / threads. Every configuration gives bitwise-identical results. */
@@ -295,22 +288,23 @@ int smpq_kl_rows(const float* p_ref, const float* p, int rows, int cols, double*
                  smpq_stream_t stream);
 
 /* ---- content fingerprints (cache validation; smpq/engine.py) ------------------------------------
- * smpq_fingerprint: out[t] = sum_i H(w_i, i) mod 2^64 over the nwords[t] 32-bit words of
- *   tensor t (device pointers ptrs[t], a device array), for t < ntensors; the work is split into
+ * smpq_fingerprint: out[t] = sum_i H(w_i, i) mod 2^64 over the ceil(nbytes[t] / 4) 32-bit words of
+ *   tensor t (device pointers ptrs[t], 4-B aligned, a device array; a partial last word is
+ *   zero-padded), for t < ntensors; the work is split into
  *   nchunks chunks of smpq_fingerprint_chunk_words() words: chunk c covers tensor chunk_tensor[c]
  *   from word chunk_word[c] (device arrays). out (device uint64 [ntensors]) is overwritten.
  *   H(w, i) = fmix32(w ^ i*0x9E3779B9) | fmix32(w ^ (i*0x85EBCA6B + 0xC2B2AE35)) << 32, fmix32 = the
  *   MurmurHash3 finalizer (all arithmetic mod 2^32): injective in w for each i, so any single-word
  *   change changes the fingerprint, and structured multi-word changes cancel with p ~ 2^-64.
  * smpq_fingerprint_compare: *flag |= 1 if a[i] != b[i] for some i < n (device arrays).
- * smpq_fingerprint_host: the same sum over host memory.
+ * smpq_fingerprint_host: the same sum over nbytes bytes of host memory.
  * Used to detect in-place writes through `.data` (functions.py:22, resnet50_main.py:191) that
  * leave a Parameter's version counter unchanged. */
 long long smpq_fingerprint_chunk_words(void);
-int smpq_fingerprint(const void* const* ptrs, const int64_t* nwords, int ntensors, const int32_t* chunk_tensor,
+int smpq_fingerprint(const void* const* ptrs, const int64_t* nbytes, int ntensors, const int32_t* chunk_tensor,
                      const int64_t* chunk_word, int nchunks, uint64_t* out, smpq_stream_t stream);
 int smpq_fingerprint_compare(const uint64_t* a, const uint64_t* b, int n, int32_t* flag, smpq_stream_t stream);
-uint64_t smpq_fingerprint_host(const void* p, int64_t nwords);
+uint64_t smpq_fingerprint_host(const void* p, int64_t nbytes);
 
 /* Diagnostics: one v_mfma_i32_16x16x64_i8 with the kernel's fragment mapping.
  *   a [16][64] int8 row-major, b [16][64] int8 (b[col][k]), c [16][16] int32 row-major */

@@ -942,8 +942,16 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
   }
   hipStream_t s = (hipStream_t)stream;
   if (tile_cfg < 0) {
-    const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
-    tile_cfg = heuristic_cfg(limbs + wlimbs - 1 - smin, M, cout, a.K, smallc);
+    // the LDS-DMA family whenever it takes the shape; the register-staged family only where it
+    // cannot (cin == 4, planes >= 2 GiB): that kernel showed a rare, unexplained limb-plane
+    // mismatch under the repeated-launch screen, so no default reaches it otherwise
+    const int g = glds_default_cfg(a, limbs, wlimbs);
+    if (g >= 0) {
+      tile_cfg = kNumTileCfgs + g;
+    } else {
+      const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
+      tile_cfg = heuristic_cfg(limbs + wlimbs - 1 - smin, M, cout, a.K, smallc);
+    }
   }
   if (tile_cfg >= kNumTileCfgs + glds_num_cfgs()) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   if (limbs < 1 || limbs > 3) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: limbs must be 1, 2 or 3");

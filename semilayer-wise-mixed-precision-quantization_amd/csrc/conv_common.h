@@ -80,6 +80,7 @@ void glds_cfg_info(int cfg, int* bm, int* bn, int* threads);
 int glds_cfg_bk(int cfg);
 bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs);
 int launch_glds(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s);
+int glds_default_cfg(const ConvArgs& a, int limbs, int wlimbs);
 
 // The 4 codes (channels 0..3) held by one dword per limb plane, w[l] = the 4 balanced digits of
 // limb l: q = sum_l d_l 256^l. With u_l = d_l + 128 (byte ^ 0x80) for the low limbs,

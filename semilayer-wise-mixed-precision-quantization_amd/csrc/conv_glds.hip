@@ -821,6 +821,24 @@ bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int w
   return lds <= 160 * 1024;
 }
 
+static bool glds_planes_ok(const ConvArgs& a, int limbs, int wlimbs) {
+  const long long lim = 0x7fffff00LL;  // operand and output planes use 32-bit buffer offsets
+  return (long long)limbs * a.plane <= lim && (long long)wlimbs * a.wplane <= lim &&
+         (long long)limbs * a.M * a.cout <= lim && !(a.residual && 4LL * a.M * a.cout > lim);
+}
+
+// Built-in tile when the caller passes -1 (the Python layer autotunes per shape instead): a
+// general 128 x 64 tile (64 x 64 for cout <= 64), else the first configuration that takes the
+// shape; -1 when no LDS-DMA configuration does.
+int glds_default_cfg(const ConvArgs& a, int limbs, int wlimbs) {
+  if (a.s2d || a.cin % kKStep != 0 || a.cout % 16 != 0 || !glds_planes_ok(a, limbs, wlimbs)) return -1;
+  const int first = a.cout <= 64 ? 3 : 2;
+  if (glds_supported(first, a.cin, a.cout, a.kh, a.kw, limbs, wlimbs)) return first;
+  for (int c = 0; c < kNumGlds; ++c)
+    if (glds_supported(c, a.cin, a.cout, a.kh, a.kw, limbs, wlimbs)) return c;
+  return -1;
+}
+
 void glds_cfg_info(int cfg, int* bm, int* bn, int* threads) {
   const GldsCfg& c = kGlds[cfg];
   *bm = 16 * c.wp * c.wavesp;  // pixels (GEMM rows)
@@ -933,10 +951,7 @@ static int launch_s2d(int cfg, const ConvArgs& a, hipStream_t s) {
 
 int launch_glds(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s) {
   // operand and output planes are addressed with 32-bit buffer offsets below kOOB
-  const long long lim = 0x7fffff00LL;
-  if ((!a.s2d && a.cin % kKStep != 0) || a.cout % 16 != 0 || (long long)limbs * a.plane > lim ||
-      (long long)wlimbs * a.wplane > lim || (long long)limbs * a.M * a.cout > lim ||
-      (a.residual && 4LL * a.M * a.cout > lim))
+  if ((!a.s2d && a.cin % kKStep != 0) || a.cout % 16 != 0 || !glds_planes_ok(a, limbs, wlimbs))
     return fail(SMPQ_E_INVALID,
                 "smpq_conv2d_fwd: LDS-DMA tile configs need cin % 64 == 0, cout % 16 == 0 and planes < 2 GiB");
   if (a.s2d) {

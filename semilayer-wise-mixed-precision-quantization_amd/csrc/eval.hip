@@ -112,6 +112,88 @@ __global__ __launch_bounds__(256) void sum_rows_kernel(const float* __restrict__
   }
 }
 
+
+// ---- AdaptiveAvgPool2d(1) + flatten + fc (resnet.py:216-218), batch-invariant ----------------
+// pooled[n][c] = (x[n][0][c] + x[n][1][c] + ... + x[n][hw-1][c]) / hw, summed in pixel order: one
+// thread per 4 channels of one image (float4 loads, consecutive threads -> consecutive channels).
+__global__ __launch_bounds__(256) void avgpool_kernel(const float* __restrict__ x, int n, int hw, int c,
+                                                      float* __restrict__ pooled) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int c4 = c / 4;
+  if (t >= (long long)n * c4) return;
+  const int img = (int)(t / c4), q = (int)(t - (long long)img * c4);
+  const float4* p = reinterpret_cast<const float4*>(x + (long long)img * hw * c) + q;
+  float4 s = p[0];
+  for (int i = 1; i < hw; ++i) {
+    const float4 v = p[(long long)i * c4];
+    s.x = __fadd_rn(s.x, v.x);
+    s.y = __fadd_rn(s.y, v.y);
+    s.z = __fadd_rn(s.z, v.z);
+    s.w = __fadd_rn(s.w, v.w);
+  }
+  const float d = (float)hw;
+  reinterpret_cast<float4*>(pooled)[t] = make_float4(__fdiv_rn(s.x, d), __fdiv_rn(s.y, d), __fdiv_rn(s.z, d),
+                                                     __fdiv_rn(s.w, d));
+}
+
+// logits[i][o] = fc_b[o] + sum_k pooled[i][k] * w[o][k], the sum as one fmaf chain over k = 0..c-1
+// (then + bias): the order depends on nothing but c, so a row's logits are the same bits in any
+// batch. Block tile: 16 images x 64 outputs, K chunks of 64 staged in LDS (k-major); thread
+// (i = t / 16, o4 = t % 16) owns outputs 4 o4 .. 4 o4 + 3 of image i.
+constexpr int kFcI = 16, kFcO = 64, kFcK = 64;
+__global__ __launch_bounds__(256) void fc_kernel(const float* __restrict__ pooled, int n, int c,
+                                                 const float* __restrict__ w, const float* __restrict__ b, int nout,
+                                                 float* __restrict__ logits) {
+  // k-major LDS images (rows padded to keep the transposing writes at <= 4-way bank conflicts)
+  __shared__ __attribute__((aligned(16))) float sp[kFcK][kFcI + 4];
+  __shared__ __attribute__((aligned(16))) float sw[kFcK][kFcO + 4];
+  const int tid = threadIdx.x;
+  const int i0 = blockIdx.y * kFcI, o0 = blockIdx.x * kFcO;
+  const int ti = tid / 16, to = tid % 16;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < c; k0 += kFcK) {
+    // 16-B loads along k (16 lanes = one 256-B row piece): pooled 16 images x 64 k (one per
+    // thread), weights 64 outputs x 64 k (four per thread)
+    {
+      const int ii = tid / 16, kq = tid % 16, img = i0 + ii, k = k0 + 4 * kq;
+      const float4 v = (img < n && k < c) ? *reinterpret_cast<const float4*>(pooled + (long long)img * c + k)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      sp[4 * kq][ii] = v.x;
+      sp[4 * kq + 1][ii] = v.y;
+      sp[4 * kq + 2][ii] = v.z;
+      sp[4 * kq + 3][ii] = v.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = tid + 256 * r, oo = e / 16, kq = e % 16, o = o0 + oo, k = k0 + 4 * kq;
+      const float4 v = (o < nout && k < c) ? *reinterpret_cast<const float4*>(w + (long long)o * c + k)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      sw[4 * kq][oo] = v.x;
+      sw[4 * kq + 1][oo] = v.y;
+      sw[4 * kq + 2][oo] = v.z;
+      sw[4 * kq + 3][oo] = v.w;
+    }
+    __syncthreads();
+    const int kn = min(kFcK, c - k0);
+    for (int kk = 0; kk < kn; ++kk) {
+      const float pv = sp[kk][ti];
+      const float4 wv = *reinterpret_cast<const float4*>(&sw[kk][4 * to]);
+      acc[0] = __fmaf_rn(pv, wv.x, acc[0]);
+      acc[1] = __fmaf_rn(pv, wv.y, acc[1]);
+      acc[2] = __fmaf_rn(pv, wv.z, acc[2]);
+      acc[3] = __fmaf_rn(pv, wv.w, acc[3]);
+    }
+    __syncthreads();
+  }
+  const int img = i0 + ti;
+  if (img >= n) return;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int o = o0 + 4 * to + j;
+    if (o < nout) logits[(long long)img * nout + o] = b ? __fadd_rn(acc[j], b[o]) : acc[j];
+  }
+}
+
 }  // namespace
 }  // namespace smpq
 
@@ -145,4 +227,23 @@ extern "C" int smpq_kl_rows(const float* p_ref, const float* p, int rows, int co
   // [0] += sum of the per-image KL terms, [1] += rows
   hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, stream, row_ws, rows, 1, 1.0, 1.0, stats, 0);
   return check_hip(hipGetLastError(), "sum_rows_kernel launch");
+}
+
+extern "C" int smpq_avgpool_fc(const float* x, int n, int hw, int c, const float* fc_w, const float* fc_b, int nout,
+                               float* pooled_ws, float* logits, smpq_stream_t stream_) {
+  hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+  if (n < 0 || hw <= 0 || c <= 0 || (c % 4) != 0 || nout <= 0 ||
+      (n > 0 && (!x || !fc_w || !pooled_ws || !logits)))
+    return fail(SMPQ_E_INVALID, "smpq_avgpool_fc: bad arguments (c % 4 == 0)");
+  if (n == 0) return SMPQ_OK;
+  if ((long long)n * hw * c > 0x7fffffffLL * 4 || n > 65535 * kFcI)
+    return fail(SMPQ_E_SHAPE, "smpq_avgpool_fc: tensor too large");
+  const long long threads = (long long)n * (c / 4);
+  hipLaunchKernelGGL(avgpool_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, x, n, hw, c,
+                     pooled_ws);
+  int rc = check_hip(hipGetLastError(), "avgpool_kernel launch");
+  if (rc) return rc;
+  hipLaunchKernelGGL(fc_kernel, dim3((nout + kFcO - 1) / kFcO, (n + kFcI - 1) / kFcI), dim3(256), 0, stream,
+                     pooled_ws, n, c, fc_w, fc_b, nout, logits);
+  return check_hip(hipGetLastError(), "fc_kernel launch");
 }

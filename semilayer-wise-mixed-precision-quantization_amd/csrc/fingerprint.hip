@@ -40,8 +40,15 @@ __host__ __device__ __forceinline__ unsigned long long word_hash(uint32_t w, uin
 }
 constexpr long long kChunkWords = 16384;  // 64 KiB per block
 
+// A tensor of nbytes bytes is hashed as ceil(nbytes / 4) words, the last one zero-padded (its
+// missing bytes masked off; tensors start 4-B aligned, so the load stays inside the allocation).
+__host__ __device__ __forceinline__ uint32_t tail_mask(long long nbytes) {
+  const int r = (int)(nbytes & 3);
+  return r == 0 ? 0xffffffffu : (0xffffffffu >> (8 * (4 - r)));
+}
+
 __global__ __launch_bounds__(kFpThreads) void fingerprint_kernel(const uint32_t* const* __restrict__ ptrs,
-                                                                   const long long* __restrict__ nwords,
+                                                                   const long long* __restrict__ nbytes,
                                                                    const int* __restrict__ chunk_tensor,
                                                                    const long long* __restrict__ chunk_word,
                                                                    unsigned long long* __restrict__ out) {
@@ -49,12 +56,16 @@ __global__ __launch_bounds__(kFpThreads) void fingerprint_kernel(const uint32_t*
   const int c = blockIdx.x;
   const int t = chunk_tensor[c];
   const long long w0 = chunk_word[c];
-  const long long n = nwords[t];
+  const long long nb = nbytes[t];
+  const long long n = (nb + 3) >> 2;
+  const uint32_t last_mask = tail_mask(nb);
   const long long w1 = w0 + kChunkWords < n ? w0 + kChunkWords : n;
   const uint32_t* p = ptrs[t];
   unsigned long long acc = 0;
   // 16-B loads where the chunk is whole quads (tensors start 16-B aligned: caching-allocator blocks)
-  const bool vec = ((reinterpret_cast<unsigned long long>(p) & 15) == 0) && ((w1 - w0) & 3) == 0;
+  // and does not hold a partial last word
+  const bool vec = ((reinterpret_cast<unsigned long long>(p) & 15) == 0) && ((w1 - w0) & 3) == 0 &&
+                   (w1 < n || last_mask == 0xffffffffu);
   if (vec) {
     const uint4* q = reinterpret_cast<const uint4*>(p + w0);
     const int nq = (int)((w1 - w0) >> 2);
@@ -64,7 +75,8 @@ __global__ __launch_bounds__(kFpThreads) void fingerprint_kernel(const uint32_t*
       acc += word_hash(v.x, i) + word_hash(v.y, i + 1u) + word_hash(v.z, i + 2u) + word_hash(v.w, i + 3u);
     }
   } else {
-    for (long long i = w0 + threadIdx.x; i < w1; i += kFpThreads) acc += word_hash(p[i], (uint32_t)i);
+    for (long long i = w0 + threadIdx.x; i < w1; i += kFpThreads)
+      acc += word_hash(i == n - 1 ? (p[i] & last_mask) : p[i], (uint32_t)i);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, kWave);
@@ -98,15 +110,15 @@ using namespace smpq;
 
 extern "C" long long smpq_fingerprint_chunk_words(void) { return kChunkWords; }
 
-extern "C" int smpq_fingerprint(const void* const* ptrs, const int64_t* nwords, int ntensors,
+extern "C" int smpq_fingerprint(const void* const* ptrs, const int64_t* nbytes, int ntensors,
                                 const int32_t* chunk_tensor, const int64_t* chunk_word, int nchunks,
                                 uint64_t* out, smpq_stream_t stream) {
-  if (!ptrs || !nwords || !chunk_tensor || !chunk_word || !out || ntensors <= 0 || nchunks <= 0)
+  if (!ptrs || !nbytes || !chunk_tensor || !chunk_word || !out || ntensors <= 0 || nchunks <= 0)
     return fail(SMPQ_E_INVALID, "smpq_fingerprint: bad arguments");
   hipLaunchKernelGGL(fingerprint_zero_kernel, dim3((ntensors + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<unsigned long long*>(out), ntensors);
   hipLaunchKernelGGL(fingerprint_kernel, dim3(nchunks), dim3(kFpThreads), 0, (hipStream_t)stream,
-                     reinterpret_cast<const uint32_t* const*>(ptrs), reinterpret_cast<const long long*>(nwords),
+                     reinterpret_cast<const uint32_t* const*>(ptrs), reinterpret_cast<const long long*>(nbytes),
                      chunk_tensor, reinterpret_cast<const long long*>(chunk_word),
                      reinterpret_cast<unsigned long long*>(out));
   return check_hip(hipGetLastError(), "fingerprint_kernel launch");
@@ -121,10 +133,15 @@ extern "C" int smpq_fingerprint_compare(const uint64_t* a, const uint64_t* b, in
   return check_hip(hipGetLastError(), "fingerprint_compare_kernel launch");
 }
 
-// Host twin (tests and CPU tensors): the same sum over one tensor's words.
-extern "C" uint64_t smpq_fingerprint_host(const void* p, int64_t nwords) {
-  const uint32_t* w = static_cast<const uint32_t*>(p);
+// Host twin (tests): the same sum over one tensor's nbytes bytes (last word zero-padded).
+extern "C" uint64_t smpq_fingerprint_host(const void* p, int64_t nbytes) {
+  const uint8_t* b = static_cast<const uint8_t*>(p);
+  const long long n = (nbytes + 3) >> 2;
   unsigned long long acc = 0;
-  for (long long i = 0; i < nwords; ++i) acc += word_hash(w[i], (uint32_t)i);
+  for (long long i = 0; i < n; ++i) {
+    uint32_t w = 0;
+    for (int k = 0; k < 4 && 4 * i + k < nbytes; ++k) w |= (uint32_t)b[4 * i + k] << (8 * k);
+    acc += word_hash(w, (uint32_t)i);
+  }
   return acc;
 }

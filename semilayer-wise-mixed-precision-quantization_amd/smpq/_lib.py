@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must be imported before the library; see module doc
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsmpq.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lib = None
 _lock = threading.Lock()
@@ -35,6 +35,7 @@ _i64 = ctypes.c_int64
 _PROTOS = {
     "smpq_abi_version": (_i, []),
     "smpq_last_error": (ctypes.c_char_p, []),
+    "smpq_build_stamp": (ctypes.c_char_p, []),
     "smpq_quantize_channels": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp]),
     "smpq_quantize_channels_host": (_i, [_vp, _i, _i, _vp, _vp]),
     "smpq_quantize_channels_ex": (_i, [_vp, _i, _i, _vp, _vp, _vp, _i, _vp]),
@@ -58,11 +59,6 @@ _PROTOS = {
                                   ctypes.c_float, _vp, _i, _vp]),
     "smpq_stem_pool_supported": (_i, [_i] * 6),
     "smpq_stem_pool_s2d_q": (_i, [_vp, _vp, _i, _i, _i, _vp, _i, _i, _vp, _vp, _i, _vp, ctypes.c_float, _vp, _vp]),
-    "smpq_bottleneck_tail_num_configs": (_i, []),
-    "smpq_bottleneck_tail_supported": (_i, [_i] * 6),
-    "smpq_bottleneck_tail_q": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i,
-                                    ctypes.c_float, _vp, _vp, _i, _vp, _vp, _vp, ctypes.c_float, _i, _i, _vp,
-                                    ctypes.c_float, _vp, _i, _vp]),
     "smpq_conv2d_num_tile_configs": (_i, []),
     "smpq_conv2d_tile_config": (_i, [_i, _vp, _vp, _vp]),
     "smpq_conv2d_tile_kind": (_i, [_i]),
@@ -71,6 +67,7 @@ _PROTOS = {
     "smpq_debug_mfma_i8": (_i, [_vp, _vp, _vp, _vp]),
     "smpq_softmax_xent": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp]),
     "smpq_kl_rows": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp]),
+    "smpq_avgpool_fc": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp]),
     "smpq_fingerprint_chunk_words": (ctypes.c_longlong, []),
     "smpq_fingerprint": (_i, [_vp, _vp, _i, _vp, _vp, _i, _vp, _vp]),
     "smpq_fingerprint_compare": (_i, [_vp, _vp, _i, _vp, _vp]),

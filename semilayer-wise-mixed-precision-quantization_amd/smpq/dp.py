@@ -2,8 +2,14 @@
 
 Images are independent units: rank r owns images [r*B/k, (r+1)*B/k) of a global batch, runs the
 whole model on them, and the logits are all-gathered once (RCCL over xGMI on the GPU box; gloo in
-the CPU tests). There is no other collective — batched ImageNet inference has no exchange step.
+the CPU tests). The data path has no other collective — batched ImageNet inference has no exchange
+step. The static-range engine adds two control collectives of a few bytes while the ranks run in
+``lockstep``: the MAX of the per-layer calibration maxima (so every rank uses the ranges of the
+whole global batch and the gathered logits equal the single-GPU logits bit for bit) and the MAX of
+the per-forward overflow / staleness flags (so the ranks recalibrate together).
 """
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -25,6 +31,21 @@ def gather_logits(local, world, out=None):
                           device=local.device)
     dist.all_gather_into_tensor(out, local)
     return out
+
+
+@contextlib.contextmanager
+def lockstep(group=None):
+    """Within this block every rank of ``group`` (default: the whole world) runs the same
+    sequence of static-range forwards on its shard of each global batch (smpq.engine
+    set_dp_group); outside it each process calibrates on its own inputs."""
+    from smpq import engine
+    old = engine.get_dp_group()
+    use = group if group is not None else (dist.group.WORLD if dist.is_initialized() else None)
+    engine.set_dp_group(use if (use is not None and dist.get_world_size(use) > 1) else None)
+    try:
+        yield
+    finally:
+        engine.set_dp_group(old)
 
 
 def sharded_forward(fn, x_global, rank, world):
@@ -53,7 +74,7 @@ def sharded_eval(net, loader, rank, world, device=None, keep_probs=True):
     dev = device or torch.device("cuda", torch.cuda.current_device())
     stats = torch.zeros(4, dtype=torch.float64, device=dev)
     probs = []
-    with torch.no_grad():
+    with torch.no_grad(), lockstep():
         for x, y in loader:
             s, e = shard_range(x.shape[0], rank, world)
             assert (e - s) * world == x.shape[0], "equal shards required (the batch mean of shard means)"

@@ -10,12 +10,12 @@ and ``Bottleneck.forward`` (resnet.py:97-116):
     (fp32 weights as 24-bit fixed point) then the pool fused with its output's quantization;
   * every block conv + its BN (+ residual add) (+ ReLU) = one ``conv2d_q`` launch; static mode:
     its epilogue writes the NEXT conv's limb planes, dynamic mode: fp32 + the per-image max|y| the
-    next conv's quantizer needs; optionally conv2 + conv3 of a Bottleneck as one launch
-    (``bottleneck_tail_q``, kept only where the autotuner finds it faster);
+    next conv's quantizer needs;
   * the downsample 1x1 conv + BN (resnet.py:188-192) reads the block input's limb planes
     (already quantized for conv1) and writes the identity (static mode: as limb planes) consumed
     by conv3's epilogue;
-  * avgpool + fc (resnet.py:216-218) stay torch ops (2 MMAC/image).
+  * avgpool + fc (resnet.py:216-218): ``ops.avgpool_fc``, summed in an order that does not depend
+    on the batch, so an image's logits are the same bits in any batch, slice or data-parallel shard.
 
 Static mode runs the batch as ``STREAMS`` slices on their own streams (or, unsliced, each
 downsample branch on a side stream), fork/join inside the captured HIP graph; every launch computes
@@ -281,58 +281,15 @@ def block_forward(blk, x, ctx=None, last=False):
     if hasattr(blk, "conv3"):  # Bottleneck (resnet.py:97-116)
         t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
 
-        def tail():
-            t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
-            join()
-            return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax,
-                            want_f32=last)
-        if not last:
-            fused = _fused_tail(blk, t1, identity, ctx, join, tail)
-            if fused is not None:
-                return fused
-        return tail()
+        t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
+        join()
+        return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax,
+                        want_f32=last)
     # BasicBlock (resnet.py:55-68)
     t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
     join()
     return run_conv(blk.conv2, blk.bn2, t1, True, residual=identity, ctx=ctx, want_amax=out_amax,
                     want_f32=last)
-
-
-def _fused_tail(blk, t1, identity, ctx, join, unfused):
-    """Static mode: conv2 + bn2 + relu + conv3 + bn3 + identity + relu of a Bottleneck
-    (resnet.py:103-114) as one launch (ops.bottleneck_tail_q: t2 stays on chip) when both convs
-    carry exact int8 codes and the autotuner finds it faster than the two launches; returns the
-    block output Act, or None for the two-launch path."""
-    if ctx is None or ctx.ranges is None or not isinstance(identity, Act) or identity.q is None \
-            or identity.f32 is not None or identity.rng is None or t1.q is None or t1.rng is None:
-        return None
-    c2, c3 = blk.conv2, blk.conv3
-    if id(c2) not in ctx.ranges or id(c3) not in ctx.ranges or c2.kernel_size[0] != c2.kernel_size[1] \
-            or c3.kernel_size != (1, 1) or c3.stride != (1, 1) or c3.padding != (0, 0):
-        return None
-    p2, p3 = conv_plan(c2, blk.bn2), conv_plan(c3, blk.bn3)
-    if p2 is None or p3 is None or p2[4] != "exact8" or p3[4] != "exact8":
-        return None
-    limbs, cmid = t1.q.shape[0], t1.q.shape[-1]
-    if c2.out_channels != cmid or c3.in_channels != cmid or c3.out_channels != 4 * cmid:
-        return None
-    box = []
-
-    def two_launches():
-        a = unfused()
-        box.append(a)
-        return a.q
-    join()  # the fused launch reads the identity (downsample branch) from its first chunk on
-    rng3 = ctx.ranges[id(c3)]
-    h0 = stats["hip_conv"]  # the autotuner may run the two-launch path several times: count 2 convs
-    yq = ops.tuned_bottleneck_tail(
-        two_launches, t1.q, t1.amax, p2[0], p2[1], c2.kernel_size[0], c2.stride[0], c2.padding[0], p2[2], p2[3],
-        ctx.ranges[id(c2)], p3[0], p3[1], p3[2], p3[3], identity.q, identity.rng, rng3, ctx.overflow)
-    stats["hip_conv"] = h0 + 2
-    if box and box[-1].q is yq:
-        return box[-1]
-    c2.last_path = c3.last_path = "hip-exact8-tail"
-    return Act(q=yq, amax=ctx.range_tensor(c3), rng=rng3)
 
 
 def stem_s2d_plan(conv, bn):
@@ -416,12 +373,22 @@ def _blocks(model):
     return [b for layer in (model.layer1, model.layer2, model.layer3, model.layer4) for b in layer]
 
 
-def _features(model, x, ctx, pool=True):
+def _head(model, feat):
+    """avgpool + flatten + fc (resnet.py:216-218) on the last block's NHWC fp32 output: the
+    batch-invariant HIP kernel for the reference's modules, torch for anything else."""
+    ap = model.avgpool
+    if isinstance(model.fc, torch.nn.Linear) and isinstance(ap, torch.nn.AdaptiveAvgPool2d) \
+            and ap.output_size in (1, (1, 1)) and feat.is_cuda and feat.shape[-1] % 4 == 0:
+        return ops.avgpool_fc(feat, model.fc.weight, model.fc.bias)
+    return model.fc(feat.mean(dim=(1, 2)))
+
+
+def _features(model, x, ctx):
     act = stem_forward(model, x, ctx)
     blocks = _blocks(model)
     for i, blk in enumerate(blocks):
         act = block_forward(blk, act, ctx, last=(i == len(blocks) - 1))
-    return act.f32.mean(dim=(1, 2)) if pool else act.f32
+    return act.f32
 
 
 def _forward(model, x, ctx):
@@ -432,8 +399,8 @@ def _forward(model, x, ctx):
     if nst > 1 and n >= 2 * nst:
         # static mode: the batch as nst concurrent slices, each on its own stream, so that one
         # slice's bandwidth-bound convs overlap another's MFMA/L2-bound ones; every image's result
-        # is the same as in the serial forward (per-layer ranges are fixed, kernels exact). With
-        # chunking (CHUNK < n) the chunks go round-robin over the nst streams instead.
+        # is the same as in the serial forward (per-layer ranges are fixed, kernels exact, the head
+        # batch-invariant). With chunking (CHUNK < n) the chunks go round-robin over the streams.
         if len(parts) == 1:
             step = (n + nst - 1) // nst
             parts = [(s, min(n, s + step)) for s in range(0, n, step)]
@@ -443,31 +410,67 @@ def _forward(model, x, ctx):
             for m in model.modules():
                 if id(m) in ctx.ranges:
                     ctx.range_tensor(m)
-        feats = []
+        logits = []
         lanes = min(nst, len(parts))
         for i in range(lanes):
             _stream((x.device, "slice", i)).wait_stream(main)
         for i, (s0, s1) in enumerate(parts):
             with torch.cuda.stream(_stream((x.device, "slice", i % lanes))):
                 ctx.n, ctx.lane = s1 - s0, i % lanes
-                feats.append(_features(model, x[s0:s1], ctx, pool=False))
+                logits.append(_head(model, _features(model, x[s0:s1], ctx)))
         for i in range(lanes):
             main.wait_stream(_stream((x.device, "slice", i)))
         ctx.n, ctx.lane = n, None
-        # avgpool over the whole batch at once: the same reduction as the serial forward
-        return model.fc(torch.cat(feats).mean(dim=(1, 2)))
+        return torch.cat(logits) if len(logits) > 1 else logits[0]
     if len(parts) == 1:
-        return model.fc(_features(model, x, ctx))
-    feats = []
+        return _head(model, _features(model, x, ctx))
+    logits = []
     for s0, s1 in parts:
         if ctx is not None:
             ctx.n = s1 - s0
-        feats.append(_features(model, x[s0:s1], ctx))
+        logits.append(_head(model, _features(model, x[s0:s1], ctx)))
     if ctx is not None:
         ctx.n = n
-    return model.fc(torch.cat(feats))
+    return torch.cat(logits)
 
 
+# ---- data-parallel group ------------------------------------------------------------------------
+# When set, every rank of this process group runs the same sequence of static-range forwards on
+# its own shard of each global batch (smpq.dp / bench.py). The per-layer maxima of a calibration
+# are MAX-all-reduced, so every rank holds the ranges a single process would calibrate on the
+# whole global batch; and every decision that starts a calibration (first use, a weight change,
+# an overflow, stale weights) is taken collectively, so the ranks never diverge. Static-range
+# logits of an image then depend only on the weights, the global batch's ranges and the image:
+# the gathered logits equal the single-GPU forward of the global batch bit for bit.
+_DP = [None]
+
+
+def set_dp_group(group):
+    """Process group (torch.distributed) of the ranks that forward shards of the same global
+    batches in lockstep, or None (default: this process calibrates on its own inputs)."""
+    _DP[0] = group
+
+
+def get_dp_group():
+    return _DP[0]
+
+
+def _dp_max_(t):
+    """In-place MAX all-reduce of ``t`` over the data-parallel group (a no-op without one)."""
+    g = _DP[0]
+    if g is None:
+        return t
+    import torch.distributed as dist
+    if t.is_cuda and dist.get_backend(g) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MAX, group=g)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g)
+    return t
+
+
+# ---- cache validity -----------------------------------------------------------------------------
 def _fp_tensors(model):
     """Tensors whose CONTENT the caches are built from: conv weights (+ bias) and quantization
     metadata (packed codes, folded scales), BN buffers / affine parameters (folded shift)."""
@@ -491,34 +494,70 @@ def _signature(model):
     return (ops.get_act_limbs(), HEADROOM, ts, convs)
 
 
-def _fresh_fingerprint(model, device):
-    """Invalidate the model's content-keyed caches (its weights are repacked and BN refolded from
-    their current values on the next use) and fingerprint the current content: caches built from
-    here on match it."""
+def _bump_content(model):
+    """Invalidate the content-keyed caches (packed codes, folded BN): rebuilt on next use."""
     for m in model.modules():
         if isinstance(m, QConv2d):
             m._content_gen += 1
-    return Fingerprinter(_fp_tensors(model), device)
 
 
-def calibrate(model, x):
-    """Dynamic forward of ``x`` that (re)sets the per-layer static ranges; returns its logits."""
-    fp = _fresh_fingerprint(model, x.device)
+def _refresh_fingerprint(model, device, stale=False):
+    """Fingerprint the current content. The content-keyed caches are invalidated only when they
+    may hold other content: ``stale`` (a fingerprint check failed) or the content differs from
+    the last fingerprint taken (model._smpq_fp, shared by both range modes; one host sync).
+    Returns (fingerprinter, whether the caches were invalidated)."""
+    fp = Fingerprinter(_fp_tensors(model), device)
+    old = getattr(model, "_smpq_fp", None)
+    changed = stale or old is None or not fp.same_content(old)
+    if changed:
+        _bump_content(model)
+    model._smpq_fp = fp
+    return fp, changed
+
+
+class Calibration:
+    """Per-layer maxima of one calibration forward (a dynamic-range forward): ``keys`` (conv ids in
+    module order), ``maxima`` (device fp32 tensor), the logits, the content fingerprint taken
+    before it and whether that forward's content differs from the previous calibration's."""
+    __slots__ = ("keys", "maxima", "logits", "fp", "changed", "sig0")
+
+
+def calibration_maxima(model, x, stale=False):
+    """Run the calibration forward of ``x`` (dynamic ranges) and return its Calibration."""
+    c = Calibration()
+    c.sig0 = _signature(model)
+    c.fp, c.changed = _refresh_fingerprint(model, x.device, stale)
     ctx = Ctx(x.shape[0], x.device, record=True)
-    y = _forward(model, x, ctx)
-    keys = list(ctx.record)
-    if keys:
-        maxima = torch.cat([ctx.record[k] for k in keys]).cpu().tolist()
-        old = getattr(model, "_smpq_ranges", None)
-        ranges = {}
-        for k, v in zip(keys, maxima):
-            r = max(v, 1e-30) * HEADROOM
-            if old is not None and old[1] == _signature(model) and k in old[0]:
-                r = max(r, old[0][k])
-            ranges[k] = r
-        model._smpq_ranges = (ranges, _signature(model), {}, fp)
+    c.logits = _forward(model, x, ctx)
+    c.keys = [id(m) for m in model.modules() if id(m) in ctx.record]
+    c.maxima = torch.cat([ctx.record[k] for k in c.keys]) if c.keys else torch.zeros(0, device=x.device)
+    return c
+
+
+def set_calibration(model, c, widen=True):
+    """Install the static ranges range_l = HEADROOM * max_l of Calibration ``c``. With ``widen``
+    and unchanged weights (same signature, same content as the previous calibration, e.g. an
+    overflow rerun) each range stays at least its previous value, so ranges only grow."""
+    maxima = c.maxima.cpu().tolist()
+    old = getattr(model, "_smpq_ranges", None)
+    keep = widen and old is not None and not c.changed and old[1] == c.sig0
+    ranges = {}
+    for k, v in zip(c.keys, maxima):
+        r = max(v, 1e-30) * HEADROOM
+        if keep and k in old[0]:
+            r = max(r, old[0][k])
+        ranges[k] = r
+    model._smpq_ranges = (ranges, _signature(model), {}, c.fp)
+
+
+def calibrate(model, x, stale=False):
+    """Dynamic forward of ``x`` that (re)sets the per-layer static ranges; returns its logits.
+    In a data-parallel group the maxima are MAX-all-reduced over the ranks first."""
+    c = calibration_maxima(model, x, stale)
+    _dp_max_(c.maxima)
+    set_calibration(model, c)
     stats["calibrations"] += 1
-    return y
+    return c.logits
 
 
 def _static_eager(model, x, cal):
@@ -566,48 +605,58 @@ def _graph_forward(model, x, cal):
     return y_static.clone(), ctx.overflow
 
 
-def _dynamic_forward(model, x, retried=False):
-    """Dynamic-range forward (batch-independent results); one host sync for the content check."""
-    sig = _signature(model)
-    st = getattr(model, "_smpq_dyn", None)
-    if st is None or st[0] != sig:
-        fp = _fresh_fingerprint(model, x.device)
-        model._smpq_dyn = st = (_signature(model), fp)
-    y = _forward(model, x, None)
-    flag = torch.zeros(1, dtype=torch.int32, device=x.device)
-    st[1].check(flag)
-    if int(flag.item()) == 0 or retried:
-        return y
-    stats["stale_reruns"] += 1
-    model._smpq_dyn = None
-    return _dynamic_forward(model, x, retried=True)
+def _dynamic_forward(model, x):
+    """Dynamic-range forward (batch-independent results); one host sync for the content check.
+    A content change seen after the forward is recomputed once from freshly packed weights; a
+    change seen again after that (weights written concurrently with the forward) raises."""
+    for attempt in range(2):
+        sig = _signature(model)
+        st = getattr(model, "_smpq_dyn", None)
+        if st is None or st[0] != sig or attempt:
+            fp, _ = _refresh_fingerprint(model, x.device, stale=attempt > 0)
+            model._smpq_dyn = st = (_signature(model), fp)
+        y = _forward(model, x, None)
+        flag = torch.zeros(1, dtype=torch.int32, device=x.device)
+        st[1].check(flag)
+        if int(flag.item()) == 0:
+            return y
+        stats["stale_reruns"] += 1
+        model._smpq_dyn = None
+    raise RuntimeError("smpq: the model's weights changed while its forward ran (twice); no stale result returned")
 
 
 def forward_fused(model, x):
     """Eval-mode forward of an smpq ResNet on the GPU; returns logits [n, num_classes]."""
     if _MODE[0] == "dynamic":
         return _dynamic_forward(model, x)
+    if torch.cuda.is_current_stream_capturing():
+        # the overflow / staleness flags need a host read after the forward
+        raise RuntimeError("smpq: the static-range forward cannot run inside a caller's graph capture "
+                           "(it replays its own HIP graph); use dynamic range mode to capture it")
     cal = getattr(model, "_smpq_ranges", None)
-    if cal is None:
-        return calibrate(model, x)
-    capturing = torch.cuda.is_current_stream_capturing()
-    if USE_GRAPH[0] and not capturing and _graph_ready(model, x, cal):
-        # fast path: replay first, then validate on the host while the GPU runs; a changed weight
-        # or BN buffer discards the result (recalibrate + recapture), so nothing stale is returned
-        y, ovf = _graph_forward(model, x, cal)
-        if _signature(model) != cal[1]:
+    if _DP[0] is not None:
+        # collective decision: every rank calibrates, or none does
+        need = torch.tensor([0 if (cal is not None and cal[1] == _signature(model)) else 1], dtype=torch.int32,
+                            device=x.device)
+        if int(_dp_max_(need).item()):
             return calibrate(model, x)
+        y, ovf = _graph_forward(model, x, cal) if USE_GRAPH[0] else _static_eager(model, x, cal)
+        _dp_max_(ovf)
     else:
-        if cal[1] != _signature(model):
+        if cal is None:
             return calibrate(model, x)
-        if USE_GRAPH[0] and not capturing:
+        if USE_GRAPH[0] and _graph_ready(model, x, cal):
+            # fast path: replay first, then validate on the host while the GPU runs; a changed
+            # weight or BN buffer discards the result (recalibrate + recapture): nothing stale
             y, ovf = _graph_forward(model, x, cal)
+            if _signature(model) != cal[1]:
+                return calibrate(model, x)
         else:
-            y, ovf = _static_eager(model, x, cal)
-    if capturing:
-        return y  # inside a caller's capture: no host read possible (flags stay on the device)
+            if cal[1] != _signature(model):
+                return calibrate(model, x)
+            y, ovf = _graph_forward(model, x, cal) if USE_GRAPH[0] else _static_eager(model, x, cal)
     overflow, stale = ovf.tolist()  # one sync: results are never silently clamped or stale
     if not overflow and not stale:
         return y
     stats["stale_reruns" if stale else "overflow_reruns"] += 1
-    return calibrate(model, x)
+    return calibrate(model, x, stale=bool(stale))

@@ -17,19 +17,25 @@ from . import _lib
 
 
 class Fingerprinter:
-    """Fingerprints of a fixed list of device tensors (fp32/int8/any dtype, contiguous)."""
+    """Fingerprints of a fixed list of device tensors (any dtype; contiguous, 4-B aligned). Every
+    byte of every tensor is covered (a partial last word is hashed zero-padded); a tensor that
+    cannot be covered raises instead of being skipped, so the staleness guarantee has no holes."""
 
     def __init__(self, tensors, device):
         lib = _lib.load()
         cw = int(lib.smpq_fingerprint_chunk_words())
-        self.tensors = [t for t in tensors if t.is_cuda and t.is_contiguous() and t.numel() > 0
-                        and (t.numel() * t.element_size()) % 4 == 0]
+        self.tensors = [t for t in tensors if t.numel() > 0]
+        for t in self.tensors:
+            if not (t.is_cuda and t.is_contiguous() and t.data_ptr() % 4 == 0):
+                raise ValueError("smpq fingerprint: tensors must be contiguous, 4-B aligned and on the GPU "
+                                 "(got %s %s on %s)" % (tuple(t.shape), t.dtype, t.device))
         self.device = device
-        ptrs, nwords, ct, cwd = [], [], [], []
+        ptrs, nbytes, ct, cwd = [], [], [], []
         for i, t in enumerate(self.tensors):
-            n = t.numel() * t.element_size() // 4
+            nb = t.numel() * t.element_size()
+            n = (nb + 3) // 4
             ptrs.append(t.data_ptr())
-            nwords.append(n)
+            nbytes.append(nb)
             for w0 in range(0, n, cw):
                 ct.append(i)
                 cwd.append(w0)
@@ -38,7 +44,8 @@ class Fingerprinter:
         if not self.enabled:
             return
         self._ptrs = torch.tensor(np.array(ptrs, dtype=np.uint64).view(np.int64), device=device)
-        self._nwords = torch.tensor(nwords, dtype=torch.int64, device=device)
+        self._nbytes = torch.tensor(nbytes, dtype=torch.int64, device=device)
+        self._layout = tuple(zip(ptrs, nbytes))
         self._ct = torch.tensor(ct, dtype=torch.int32, device=device)
         self._cw = torch.tensor(cwd, dtype=torch.int64, device=device)
         self.ref = torch.empty(self.n, dtype=torch.int64, device=device)
@@ -48,10 +55,17 @@ class Fingerprinter:
     def compute(self, out):
         lib = _lib.load()
         with torch.cuda.device(self.device):
-            _lib.check(lib.smpq_fingerprint(_lib.ptr(self._ptrs), _lib.ptr(self._nwords), self.n, _lib.ptr(self._ct),
+            _lib.check(lib.smpq_fingerprint(_lib.ptr(self._ptrs), _lib.ptr(self._nbytes), self.n, _lib.ptr(self._ct),
                                             _lib.ptr(self._cw), int(self._ct.numel()), _lib.ptr(out),
                                             _lib.stream_ptr()), "smpq_fingerprint")
         return out
+
+    def same_content(self, other):
+        """True when ``other`` fingerprints the same tensors (addresses and sizes) and their
+        content was the same then as now (one host sync)."""
+        if not self.enabled or not other.enabled:
+            return self.enabled == other.enabled
+        return self._layout == other._layout and bool(torch.equal(self.ref, other.ref))
 
     def check(self, flag):
         """Enqueue: flag (device int32 [1]) |= 1 if any tensor's bytes differ from the reference."""
@@ -67,4 +81,4 @@ class Fingerprinter:
 def host_fingerprint(t):
     """The same fingerprint of a host tensor (tests)."""
     t = t.contiguous()
-    return int(_lib.load().smpq_fingerprint_host(ctypes.c_void_p(t.data_ptr()), t.numel() * t.element_size() // 4))
+    return int(_lib.load().smpq_fingerprint_host(ctypes.c_void_p(t.data_ptr()), t.numel() * t.element_size()))

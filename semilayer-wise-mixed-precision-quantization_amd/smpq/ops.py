@@ -508,120 +508,6 @@ def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, 
                     want_f32=want_f32, residual_q=residual_q, residual_range=residual_range)
 
 
-# ---- fused Bottleneck tail: conv2 -> bn2 -> relu -> conv3 -> bn3 -> += identity -> relu ----------
-def tail_configs():
-    return range(_lib.load().smpq_bottleneck_tail_num_configs())
-
-
-def tail_supported(cfg, cmid, cout3, kh, limbs):
-    return bool(_lib.load().smpq_bottleneck_tail_supported(int(cfg), int(cmid), int(cout3), int(kh), int(kh),
-                                                           int(limbs)))
-
-
-def bottleneck_tail_q(xq, x_absmax, codes2, offset2, kh, stride, pad, col_scale2, col_shift2, range2,
-                      codes3, offset3, col_scale3, col_shift3, residual_q, residual_range, emit_range, overflow,
-                      tile_cfg, relu2=True, relu3=True):
-    """Bottleneck.forward's conv2 + bn2 + relu + conv3 + bn3 + residual + relu (resnet.py:103-114) in
-    one launch, static-range mode: t1's limb planes xq [L, n, h, w, cmid] -> the block output's limb
-    planes [L, n, ho, wo, 4 cmid] (range ``emit_range``); t2 (range ``range2``) never leaves the
-    CU. Bitwise identical to conv2d_q(conv2, emit_range=range2) then conv2d_q(conv3, residual_q=...)."""
-    _req(xq.is_cuda and xq.dtype == torch.int8 and xq.dim() == 5 and xq.is_contiguous(), "tail: xq")
-    limbs, n, h, w, cmid = xq.shape
-    if codes2.dim() == 3:
-        _req(codes2.shape[0] == 1, "tail: conv2 must have one weight limb (quantized codes)")
-        codes2 = codes2[0]
-    if codes3.dim() == 3:
-        _req(codes3.shape[0] == 1, "tail: conv3 must have one weight limb (quantized codes)")
-        codes3 = codes3[0]
-    _req(codes2.shape == (cmid, kh * kh * cmid) and codes2.dtype == torch.int8 and codes2.is_contiguous(),
-         "tail: conv2 codes shape")
-    cout3 = codes3.shape[0]
-    _req(codes3.shape == (cout3, cmid) and codes3.dtype == torch.int8 and codes3.is_contiguous(), "tail: conv3 codes")
-    for t, c in ((col_scale2, cmid), (col_shift2, cmid), (col_scale3, cout3), (col_shift3, cout3)):
-        _req(t.dtype == torch.float32 and t.numel() == c and t.is_contiguous() and t.device == xq.device,
-             "tail: col vectors")
-    for o, c in ((offset2, cmid), (offset3, cout3)):
-        _req(o is None or (o.dtype == torch.int32 and o.numel() == c), "tail: offsets")
-    ho = (h + 2 * pad - kh) // stride + 1
-    wo = (w + 2 * pad - kh) // stride + 1
-    _req(residual_q.shape == (limbs, n, ho, wo, cout3) and residual_q.dtype == torch.int8
-         and residual_q.is_contiguous(), "tail: residual_q")
-    _req(overflow is not None and overflow.dtype == torch.int32 and overflow.device == xq.device, "tail: overflow")
-    yq = torch.empty(limbs, n, ho, wo, cout3, dtype=torch.int8, device=xq.device)
-    lib = _lib.load()
-    hook = _CONV_HOOK[0]
-    if hook is not None:
-        hook.begin()
-    with torch.cuda.device(xq.device):
-        _lib.check(lib.smpq_bottleneck_tail_q(
-            _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, cmid, _lib.ptr(codes2), _lib.ptr(offset2), kh, kh, stride,
-            pad, _lib.ptr(col_scale2), _lib.ptr(col_shift2), 1 if relu2 else 0, float(range2), _lib.ptr(codes3),
-            _lib.ptr(offset3), cout3, _lib.ptr(col_scale3), _lib.ptr(col_shift3), _lib.ptr(residual_q),
-            float(residual_range), 1 if relu3 else 0, int(limbs), _lib.ptr(yq), float(emit_range),
-            _lib.ptr(overflow), int(tile_cfg), _lib.stream_ptr()), "smpq_bottleneck_tail_q")
-    if hook is not None:
-        w2 = alg_work(n, h, w, cmid, cmid, kh, kh, ho, wo, limbs, 1, False, False, False, False)
-        w3 = alg_work(n, ho, wo, cmid, cout3, 1, 1, ho, wo, limbs, 1, False, True, False, True)
-        hook.end({"ops": w2["ops"] + w3["ops"], "passes": w2["passes"],
-                  # t2 stays on chip: conv2's input + both weights + conv3's residual and output
-                  "bytes": w2["bytes"] + w3["bytes"] - limbs * n * ho * wo * cmid,
-                  "shape": "%4d->%4d->%4d k%d %3d->%3d tail" % (cmid, cmid, cout3, kh, h, ho)})
-    return yq
-
-
-TAIL_FUSION = [os.environ.get("SMPQ_TAIL", "1") != "0"]
-TAIL_FORCE = [None]  # tests: a tile config index to use wherever supported (no timing), or None
-_TUNED_TAIL = {}
-
-
-def tuned_bottleneck_tail(unfused, xq, x_absmax, codes2, offset2, kh, stride, pad, col_scale2, col_shift2, range2,
-                          codes3, offset3, col_scale3, col_shift3, residual_q, residual_range, emit_range, overflow):
-    """The fused tail with the fastest tile config for this shape, or ``unfused()`` (the two-launch
-    path, which returns the same planes) when that is faster or no config takes the shape. Timed
-    once per shape (cf. cudnn.benchmark=True, resnet50_main.py:10), then cached."""
-    limbs, n, h, w, cmid = xq.shape
-    cout3 = codes3.shape[-2]
-    key = (n, h, w, cmid, kh, stride, pad, cout3, limbs)
-    cfg = _TUNED_TAIL.get(key)
-    if TAIL_FORCE[0] is not None:
-        cands = [c for c in tail_configs() if tail_supported(c, cmid, cout3, kh, limbs)]
-        cfg = (TAIL_FORCE[0] if TAIL_FORCE[0] in cands else cands[0]) if (cands and TAIL_FUSION[0]) else -1
-    elif cfg is None:
-        cands = [c for c in tail_configs() if tail_supported(c, cmid, cout3, kh, limbs)]
-        if not TAIL_FUSION[0] or not cands:
-            cfg = -1
-        elif torch.cuda.is_current_stream_capturing() or not AUTOTUNE[0]:
-            return unfused()  # decided on the next eager call
-        else:
-            def run(c):
-                if c < 0:
-                    return unfused()
-                return bottleneck_tail_q(xq, x_absmax, codes2, offset2, kh, stride, pad, col_scale2, col_shift2,
-                                         range2, codes3, offset3, col_scale3, col_shift3, residual_q,
-                                         residual_range, emit_range, overflow, c)
-            best = None
-            for c in [-1] + cands:
-                times = []
-                for rep in range(3):
-                    e0 = torch.cuda.Event(enable_timing=True)
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                    run(c)
-                    e1.record()
-                    times.append((e0, e1))
-                torch.cuda.synchronize()
-                t = min(a.elapsed_time(b) for a, b in times[1:])
-                if best is None or t < best[0]:
-                    best = (t, c)
-            cfg = best[1]
-        _TUNED_TAIL[key] = cfg
-    if cfg < 0:
-        return unfused()
-    return bottleneck_tail_q(xq, x_absmax, codes2, offset2, kh, stride, pad, col_scale2, col_shift2, range2,
-                             codes3, offset3, col_scale3, col_shift3, residual_q, residual_range, emit_range,
-                             overflow, cfg)
-
-
 def conv2d_nhwc(x, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
                 residual=None, relu=False, limbs=None, y_absmax=None, out=None):
     """act_quantize + (autotuned) conv2d_q on an NHWC fp32 input."""
@@ -703,3 +589,25 @@ def kl_rows(p_ref, p, stats):
     with torch.cuda.device(p.device):
         _lib.check(_lib.load().smpq_kl_rows(_lib.ptr(p_ref), _lib.ptr(p), rows, cols, _lib.ptr(stats), _lib.ptr(ws),
                                             _lib.stream_ptr()), "smpq_kl_rows")
+
+
+def avgpool_fc(x_nhwc, weight, bias):
+    """AdaptiveAvgPool2d(1) + flatten + Linear (resnet.py:216-218) on the last block's NHWC fp32
+    output [n, h, w, c] -> logits [n, nout] fp32. Each logit is summed in an order fixed by c alone
+    (smpq_avgpool_fc), so an image's logits are the same bits in any batch or data-parallel shard."""
+    _req(x_nhwc.is_cuda and x_nhwc.dtype == torch.float32 and x_nhwc.dim() == 4 and x_nhwc.is_contiguous(),
+         "avgpool_fc: need contiguous NHWC fp32 on the GPU")
+    n, h, w, c = x_nhwc.shape
+    _req(c % 4 == 0, "avgpool_fc: channels must be a multiple of 4")
+    wt = weight.detach().float().contiguous()
+    _req(wt.dim() == 2 and wt.shape[1] == c and wt.device == x_nhwc.device, "avgpool_fc: weight shape")
+    nout = wt.shape[0]
+    b = None if bias is None else bias.detach().float().contiguous()
+    _req(b is None or (b.numel() == nout and b.device == x_nhwc.device), "avgpool_fc: bias")
+    pooled = torch.empty(n, c, dtype=torch.float32, device=x_nhwc.device)
+    out = torch.empty(n, nout, dtype=torch.float32, device=x_nhwc.device)
+    with torch.cuda.device(x_nhwc.device):
+        _lib.check(_lib.load().smpq_avgpool_fc(_lib.ptr(x_nhwc), n, h * w, c, _lib.ptr(wt), _lib.ptr(b), nout,
+                                               _lib.ptr(pooled), _lib.ptr(out), _lib.stream_ptr()),
+                   "smpq_avgpool_fc")
+    return out

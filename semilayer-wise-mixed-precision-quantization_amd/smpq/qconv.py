@@ -154,6 +154,13 @@ class QConv2d(nn.Conv2d):
         self._pack = (key, res)
         return res
 
+    def _s2d_stem(self, x):
+        """The 7x7/2/3 stem on <= 4 channels with every channel unquantized and even h, w."""
+        return (self.in_channels <= 4 and self.kernel_size == (7, 7) and self.stride == (2, 2)
+                and self.padding == (3, 3) and self.groups == 1 and self.dilation == (1, 1)
+                and self.out_channels % 16 == 0 and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0
+                and not (self._bits_host > 0).any())
+
     # ---- forward (module path; the fused ResNet path is smpq.engine) ------------------------
     def forward(self, x):
         if not x.is_cuda:
@@ -169,6 +176,23 @@ class QConv2d(nn.Conv2d):
             stats["fixed_conv"] += 1
         self.last_path = "hip-" + kind
         x = x.float()
+        if self._s2d_stem(x):
+            # the reference's 7x7/2/3 stem (resnet.py:143): space-to-depth planes on the LDS-DMA
+            # kernel, the same codes and results as the engine's stem (engine.stem_s2d_plan)
+            xc = x.contiguous()
+            amax = ops.act_absmax(xc)
+            xq = ops.image_quantize_s2d(xc, amax)
+            key = self._pack_key()
+            cached = getattr(self, "_s2d_pack", None)
+            if cached is None or cached[0] != key:
+                cached = self._s2d_pack = (key,) + ops.pack_weights_s2d(self.weight.detach().float(),
+                                                                       max(2, ops.get_act_limbs()))
+            codes, s2d_scale = cached[1], cached[2]
+            shift = self.bias.detach().float().contiguous() if self.bias is not None else \
+                torch.zeros(self.out_channels, dtype=torch.float32, device=x.device)
+            y = ops.tuned_stem_conv_s2d(xq, amax, codes, x.shape[2], x.shape[3], s2d_scale.contiguous(), shift,
+                                        relu=False)
+            return y.permute(0, 3, 1, 2)
         if self.in_channels <= 4:
             xc = x.contiguous()
             amax = ops.act_absmax(xc)

@@ -272,8 +272,14 @@ def bn_recalibrate(net, seed_affine=2, seed_data=3, passes=2, batch=64):
             m.momentum = 0.1
 
 
-def make_model_goldens(functions, resnet, assigns):
+def make_model_goldens(functions, resnet, assigns, only=None):
+    """Seeded-model logits of the reference's CPU forward. ``only``: regenerate just these cases
+    and merge them into the existing model_goldens.npz (the other cases are left as they are)."""
     out = {}
+    path = os.path.join(HERE, "model_goldens.npz")
+    if only:
+        with np.load(path, allow_pickle=False) as old:
+            out = {k: old[k] for k in old.files if k.split("/")[0] not in only}
     torch.set_num_threads(os.cpu_count())
     cases = [
         # name, arch, assignment, batch, recalibrate
@@ -283,8 +289,11 @@ def make_model_goldens(functions, resnet, assigns):
         ("r34_4bit", "resnet34", "r34_4bit", 2, False),
         ("r18_u8_cal", "resnet18", "r18_u8", 16, True),
         ("r50_mixed_cal", "resnet50", "r50_mixed", 8, True),
+        ("r34_4bit_cal", "resnet34", "r34_4bit", 8, True),
     ]
     for name, arch, aname, batch, cal in cases:
+        if only and name not in only:
+            continue
         torch.manual_seed(0)
         net = getattr(resnet, arch)(pretrained=False)
         net.eval()
@@ -309,7 +318,7 @@ def make_model_goldens(functions, resnet, assigns):
             logits = net(x)
         out["%s/logits" % name] = logits.numpy()
         print(name, "logits", tuple(logits.shape), "top1", logits.argmax(1)[:8].tolist())
-    np.savez_compressed(os.path.join(HERE, "model_goldens.npz"), **out)
+    np.savez_compressed(path, **out)
 
 
 def make_eval_golden(functions):
@@ -370,6 +379,11 @@ def main():
         return
     if sys.argv[1:] == ["grouping"]:
         make_grouping_golden(functions)
+        return
+    if sys.argv[1:2] == ["models"]:  # e.g. `models r34_4bit_cal`: (re)make only these cases
+        assigns = {"r50_mixed": reconstruct_r50_mixed(), "r18_u8": r18_uniform8(),
+                   "r34_4bit": r34_4bit_dominant()}
+        make_model_goldens(functions, resnet, assigns, only=set(sys.argv[2:]))
         return
     make_eval_golden(functions)
     make_grouping_golden(functions)

@@ -126,3 +126,64 @@ def test_sharded_eval_stats_all_reduce_equals_single_process():
         assert res[r] == res[0]
         assert abs(correct / seen - acc) < 1e-12
         assert abs(loss_sum / count - loss) < 1e-9
+
+
+def _calib_worker(rank, world, port, q):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "semilayer-wise-mixed-precision-quantization_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import resnet
+        from smpq import dp, engine
+        from smpq.qconv import QConv2d
+        torch.manual_seed(0)
+        net = resnet.resnet18()
+        convs = [m for m in net.modules() if isinstance(m, QConv2d)]
+        # this rank's per-layer calibration maxima (its shard of the global batch)
+        g = torch.Generator().manual_seed(100 + rank)
+        c = engine.Calibration()
+        c.keys = [id(m) for m in convs]
+        c.maxima = torch.rand(len(convs), generator=g) * (1 + rank)
+        c.logits, c.fp, c.changed, c.sig0 = None, None, True, None
+        local = c.maxima.clone()
+        with dp.lockstep():
+            assert engine.get_dp_group() is not None
+            engine._dp_max_(c.maxima)
+            # the collective decision: one rank's flag makes every rank recalibrate
+            need = torch.tensor([1 if rank == world - 1 else 0], dtype=torch.int32)
+            engine._dp_max_(need)
+        assert engine.get_dp_group() is None
+        engine.set_calibration(net, c)
+        ranges = [net._smpq_ranges[0][k] for k in c.keys]
+        q.put((rank, local, ranges, int(need.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_calibration_maxima_all_reduced_across_ranks():
+    """Data-parallel static ranges (engine.set_dp_group / dp.lockstep): every rank ends with the
+    ranges HEADROOM * (max over ranks of its per-layer maxima) = the single-process calibration of
+    the global batch, and a recalibration decision on any rank is taken by all."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_calib_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (loc, rng, need)) for r, loc, rng, need in (q.get(timeout=180) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "semilayer-wise-mixed-precision-quantization_amd"))
+    from smpq import engine
+    gmax = torch.maximum(res[0][0], res[1][0])
+    want = [max(v, 1e-30) * engine.HEADROOM for v in gmax.tolist()]
+    for r in range(world):
+        assert res[r][1] == want
+        assert res[r][2] == 1

@@ -23,7 +23,40 @@ def test_library_exports_every_header_symbol(built_lib):
     for s in syms:
         assert hasattr(built_lib, s), s
         assert s in _lib.EXPORTED_SYMBOLS, s
-    assert built_lib.smpq_abi_version() == 1
+    assert built_lib.smpq_abi_version() == 2
+
+
+def test_loaded_library_matches_the_sources(built_lib):
+    """Content-addressed build: the loaded libsmpq.so carries the SHA-256 of exactly the sources,
+    headers and flags in this tree (a stale binary cannot pass as current)."""
+    import __graft_entry__ as ge
+    stamp = ge.source_stamp()
+    assert re.fullmatch(r"[0-9a-f]{64}", stamp)
+    assert built_lib.smpq_build_stamp().decode() == stamp
+    assert ge.library_stamp() == stamp
+
+
+def test_source_stamp_tracks_content(tmp_path, monkeypatch):
+    """The stamp changes with any byte of a source or with the flags, and not with mtimes."""
+    import shutil
+    import __graft_entry__ as ge
+    base = ge.source_stamp()
+    csrc = tmp_path / "csrc"
+    shutil.copytree(ge.CSRC, csrc)
+    (tmp_path / "include").mkdir()
+    shutil.copy(ge.PUBLIC_HEADER, tmp_path / "include" / "smpq.h")
+    monkeypatch.setattr(ge, "CSRC", str(csrc))
+    monkeypatch.setattr(ge, "PUBLIC_HEADER", str(tmp_path / "include" / "smpq.h"))
+    monkeypatch.setattr(ge, "REPO", str(tmp_path))
+    same = ge.source_stamp()
+    os.utime(csrc / "eval.hip", (0, 0))
+    assert ge.source_stamp() == same
+    with open(csrc / "eval.hip", "a") as f:
+        f.write("\n")
+    assert ge.source_stamp() != same
+    monkeypatch.setattr(ge, "FLAGS", ge.FLAGS + ["-DX"])
+    assert ge.source_stamp() != same
+    assert base  # (the tree's own stamp is unaffected: the copy lives in tmp_path)
 
 
 def test_host_quantizer_bitexact_vs_reference(built_lib):

@@ -146,6 +146,23 @@ def test_torch_oracle_reproduces_reference_logits():
         assert np.abs(out - ref).max() <= 1e-5 * np.abs(ref).max()
 
 
+@pytest.mark.parametrize("case,arch,assign", [("r18_u8_cal", "resnet18", "r18_u8"),
+                                              ("r34_4bit_cal", "resnet34", "r34_4bit"),
+                                              ("r50_mixed_cal", "resnet50", "r50_mixed")])
+def test_torch_oracle_reproduces_recalibrated_reference_logits(case, arch, assign):
+    """The oracle the full-size GPU parity tests compare against (oracle/torch_ref.py) reproduces
+    the reference's own logits on the BN-recalibrated parity models of all three bench archs."""
+    from oracle import torch_ref
+    g = _goldens()
+    sd = {k: torch.from_numpy(v) for k, v in seeded_state(arch, assign, cal=case).items()}
+    ref = g[case + "/logits"]
+    x = torch.randn(ref.shape[0], 3, 224, 224, generator=torch.Generator().manual_seed(1))
+    np.testing.assert_allclose([x.double().sum().item(), x.double().abs().sum().item()], g[case + "/xsum"], rtol=1e-12)
+    out = torch_ref.resnet_forward(arch, sd, x).numpy()
+    assert np.abs(out - ref).max() <= 1e-5 * np.abs(ref).max()
+    assert (out.argmax(1) == ref.argmax(1)).all()
+
+
 def _eval_golden():
     z = np.load(os.path.join(GOLDEN, "eval_golden.npz"), allow_pickle=False)
     cuts = np.cumsum([0] + list(z["sizes"]))
