@@ -1102,7 +1102,7 @@ def test_device_fingerprint_matches_host(gpu):
 
 
 # per-image bound: max_c |logit - ref| / max_c |ref| of every single image
-PER_IMAGE_RTOL = 1e-3
+PER_IMAGE_RTOL = 2e-4
 
 
 @pytest.mark.parametrize("case,arch,assign,batch", [
