@@ -745,6 +745,7 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 }
 
 // ------------------------------------------------------------------------------------------
+#ifndef SMPQ_KERNEL_ONLY  // (tools/isa.sh compiles single kernel instances for inspection)
 struct GldsCfg {
   int wavesc, wavesp, wc, wp, stages, bk, pipe;
 };
@@ -975,4 +976,5 @@ int launch_glds(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s
   }
 }
 
+#endif  // SMPQ_KERNEL_ONLY
 }  // namespace smpq

@@ -4,8 +4,10 @@ torch itself on GPU tensors, over the inputs of quant_kat.npz.
 The reference's drivers quantize weights that already live on the GPU (evaluate_acc_loss_softmax
 moves the net with net.to(device), functions.py:97, before the search loop quantizes channels of
 it, e.g. resnet50_main.py:189-197). On a device tensor torch evaluates ``t / scale`` (scale a
-Python float) as ``t * (1.0f / fl32(scale))`` — a reciprocal multiply that can differ from the
-CPU's IEEE division by one ulp and flip rint() at a .5 boundary. This script records what torch
+Python float) as ``t * fl32(1.0 / scale)`` — a multiply by the reciprocal of the DOUBLE scale,
+rounded to fp32 once (not ``1.0f / fl32(scale)``: over this file's 71 cases the former matches
+all of them and the latter misses 4) — which can differ from the CPU's IEEE division by one ulp
+and flip rint() at a .5 boundary. This script records what torch
 produces there, so the device kernel's semantics are pinned by torch's own device arithmetic.
 
 Run on the GPU box (the reference itself does not travel; the formula below is functions.py:35-41

@@ -17,7 +17,10 @@ s32 = np.float32(s)
 tn = t.numpy()
 dev = (t.cuda() / s).cpu().numpy()
 out["div_dev_eq_ieee"] = int((dev == (tn / s32)).sum())
-out["div_dev_eq_recip"] = int((dev == (tn * (np.float32(1) / s32))).sum())
+# the two candidate reciprocals: of the fp32 scale (1.0f / fl32(s)) and of the double scale
+# rounded once (fl32(1.0 / s), what smpq implements as SMPQ_QSEM_DEVICE)
+out["div_dev_eq_recip_of_fl32_scale"] = int((dev == (tn * (np.float32(1) / s32))).sum())
+out["div_dev_eq_fl32_recip_of_double_scale"] = int((dev == (tn * np.float32(1.0 / s))).sum())
 out["div_n"] = int(tn.size)
 q = (t / s).round()
 out["add_dev_eq_cpu"] = bool(torch.equal((q.cuda() + (-107)).cpu(), q + (-107)))
