@@ -184,7 +184,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
     ap.add_argument("--config", default="r50_mixed", choices=sorted(CONFIGS))
     ap.add_argument("--limbs", type=int, default=3,
@@ -248,7 +248,10 @@ def main():
     # depends on the batch and the shard's first image only
     s0, s1 = dp.shard_range(args.batch * world, rank, world)
     xs = []
-    for b in range(max(1, args.batches)):
+    # every batch gets its graph (captured on its own input memory) within the W warm-up steps:
+    # the first warm-up step calibrates, each further one captures one batch's graph
+    nb = max(1, min(args.batches, args.warmup - 1)) if args.warmup > 1 else 1
+    for b in range(nb):
         g = torch.Generator(device=dev).manual_seed(1000 + 1000003 * b + s0)
         xs.append(torch.randn(s1 - s0, 3, 224, 224, generator=g, device=dev))
     gathered = torch.empty(world * args.batch, 1000, device=dev) if world > 1 else None

@@ -860,13 +860,12 @@ static int heuristic_cfg(int nacc, long M, int cout, int K, bool smallc) {
 
 using namespace smpq;
 
-extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+static int conv_args_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                                  const int8_t* codes, int wlimbs, const int32_t* offset, int cout, int kh,
                                  int kw, int stride, int pad, const float* col_scale,
                                  const float* col_shift, const float* residual, int relu, int limbs,
                                  float* y, float* y_absmax, int8_t* yq, float yq_range, int32_t* overflow,
-                                 const int8_t* residual_q, float residual_range, int tile_cfg,
-                                 smpq_stream_t stream) {
+                                 const int8_t* residual_q, float residual_range, ConvArgs& a) {
   if (!xq || !x_absmax || !codes || !col_scale || !col_shift || (!y && !yq))
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: null pointer");
   if (yq && (!overflow || !(yq_range > 0.f)))
@@ -884,7 +883,7 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
   if (wlimbs < 1 || wlimbs > 3) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: wlimbs must be 1, 2 or 3");
   if (wlimbs == 3 && limbs != 3)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: 3 weight limbs are built for 3 activation limbs only");
-  ConvArgs a = {};
+  a = ConvArgs{};
   a.s2d = 0;
   a.xq = xq;
   a.plane = (long long)n * h * w * cin;
@@ -940,6 +939,25 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
     }();
     a.nt_store = (yq && (long long)limbs * M * cout >= nt_min) ? 1 : 0;
   }
+  if (limbs < 1 || limbs > 3) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: limbs must be 1, 2 or 3");
+  a.inv_qmax = 1.f / (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f));
+  return SMPQ_OK;
+}
+
+extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+                                 const int8_t* codes, int wlimbs, const int32_t* offset, int cout, int kh,
+                                 int kw, int stride, int pad, const float* col_scale,
+                                 const float* col_shift, const float* residual, int relu, int limbs,
+                                 float* y, float* y_absmax, int8_t* yq, float yq_range, int32_t* overflow,
+                                 const int8_t* residual_q, float residual_range, int tile_cfg,
+                                 smpq_stream_t stream) {
+  ConvArgs a;
+  const int rc = conv_args_q(xq, x_absmax, n, h, w, cin, codes, wlimbs, offset, cout, kh, kw, stride, pad, col_scale,
+                             col_shift, residual, relu, limbs, y, y_absmax, yq, yq_range, overflow, residual_q,
+                             residual_range, a);
+  if (rc) return rc;
+  const bool smallc = cin == 4;
+  const long M = a.M;
   hipStream_t s = (hipStream_t)stream;
   if (tile_cfg < 0) {
     // the LDS-DMA family whenever it takes the shape; the register-staged family only where it
@@ -954,8 +972,6 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
     }
   }
   if (tile_cfg >= kNumTileCfgs + glds_num_cfgs()) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
-  if (limbs < 1 || limbs > 3) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: limbs must be 1, 2 or 3");
-  a.inv_qmax = 1.f / (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f));
   if (tile_cfg >= kNumTileCfgs) {
     if (smallc) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: LDS-DMA tile configs need cin % 64 == 0");
     return launch_glds(tile_cfg - kNumTileCfgs, limbs, wlimbs, a, s);

@@ -50,9 +50,10 @@ constexpr int kAblate = SMPQ_DIAG_ABLATE;
 // fp32 residual, no per-image maxima): the output quantizer's 1/step is folded into the column
 // scale / shift and the residual scale, ReLU and the code clamp are one v_med3, and overflow is
 // tracked on the rounded codes — about half the VALU work of the general epilogue per output.
+// The body of one block (block `bid` of `total` blocks of this conv); `lds` = the dynamic LDS.
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
           bool LEAN = false, bool PIPE = false>
-__global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kernel(ConvArgs a) {
+__device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, int8_t* lds) {
   static_assert(BK == 64 || BK == 128, "BK");
   static_assert(!S2D || BK == 64, "the s2d stem uses 64-B K steps");
   constexpr int NW = WAVES_C * WAVES_P;
@@ -74,7 +75,6 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
   // staged in the operand area and copied out row-major (whole lines when BC >= 128 or BC == cout)
   constexpr bool TRT = (WC % 4) == 0;
   constexpr int TILEB = L * BP * BC;
-  extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // min(NST, ksteps) stages
   if constexpr ((kAblate & 32) != 0) {  // diagnostic: static-range epilogue only
     a.y = nullptr;
     a.residual = nullptr;
@@ -88,9 +88,8 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
 
   // ---- XCD-aware tile order ----------------------------------------------------------------
   const int ntc = (a.cout + BC - 1) / BC;
-  const int total = (int)gridDim.x;
   const int full = total & ~7;
-  int t = blockIdx.x;
+  int t = bid;
   if (t < full) t = (t & 7) * (full >> 3) + (t >> 3);
   const int tq = fast_div(t, a.ntc_mul, a.ntc_shr);  // t / ntc
   const int m0 = tq * BP;
@@ -742,6 +741,13 @@ __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kerne
     const bool ovf = LEAN ? vmax > qmax : rintf(__fmul_rn(vmax, a.yq_inv)) > qmax;
     if (__any(ovf) && lane == 0) atomicMax(a.overflow, 1);
   }
+}
+
+template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
+          bool LEAN = false, bool PIPE = false>
+__global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // min(NST, ksteps) stages
+  qconv_glds_body<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, LEAN, PIPE>(a, blockIdx.x, gridDim.x, lds);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -74,6 +74,7 @@ _PROTOS = {
     "smpq_fingerprint_host": (ctypes.c_uint64, [_vp, _i64]),
 }
 
+
 EXPORTED_SYMBOLS = tuple(_PROTOS)
 
 

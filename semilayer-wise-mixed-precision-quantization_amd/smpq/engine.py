@@ -247,12 +247,13 @@ def block_forward(blk, x, ctx=None, last=False):
     (avgpool): the identity of a block without downsample is read from its input's limb planes.
 
     Static mode: the downsample branch (resnet.py:188-192) depends only on the block input, so it
-    runs on a side stream concurrently with conv1 (and conv2) and joins before the conv that adds
-    it (fork/join inside the captured graph); every launch computes exactly what it computes
-    serially, so the result is bitwise the same (tests/test_gpu.py)."""
+    runs beside conv1: outside batch slices on a side stream that joins before the conv that adds
+    it (fork/join inside the captured graph); a single launch holding both convs was measured
+    slower than the two launches (profiles/r03_pair_bench.txt). Every conv computes exactly what
+    it computes serially, so the result is bitwise the same (tests/test_gpu.py)."""
     side = None
     # (not inside a batch slice: a fork nested in a slice's fork crashes hipStreamEndCapture on
-    # ROCm 7.2 / torch 2.10 — tools/debug_streams.py recap_ds_sl)
+    # ROCm 7.2 / torch 2.10 — reproduced with torch alone by tools/repro_nested_fork.py)
     if blk.downsample is not None and CONCURRENT_DS[0] and ctx is not None and ctx.ranges is not None \
             and ctx.lane is None and x.q is not None:  # both branches read the input's limb planes
         main = torch.cuda.current_stream()
@@ -278,15 +279,13 @@ def block_forward(blk, x, ctx=None, last=False):
         if side is not None:
             torch.cuda.current_stream().wait_stream(side)
 
+    t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
     if hasattr(blk, "conv3"):  # Bottleneck (resnet.py:97-116)
-        t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
-
         t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
         join()
         return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax,
                         want_f32=last)
     # BasicBlock (resnet.py:55-68)
-    t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
     join()
     return run_conv(blk.conv2, blk.bn2, t1, True, residual=identity, ctx=ctx, want_amax=out_amax,
                     want_f32=last)
@@ -573,33 +572,66 @@ def _graph_key(model, x, cal):
 
 
 def _graph_ready(model, x, cal):
+    key = _graph_key(model, x, cal)
+    per_ptr = getattr(model, "_smpq_graphs", None)
+    if per_ptr is not None and (key, x.data_ptr()) in per_ptr:
+        return True
     entry = getattr(model, "_smpq_graph", None)
-    return entry is not None and entry[0] == _graph_key(model, x, cal)
+    return entry is not None and entry[0] == key
+
+
+# HIP graphs captured on an input tensor's own memory (no copy of the input into the graph's static
+# buffer): up to this many distinct input addresses per model (an evaluation loop's input buffers
+# recycle a few addresses); further inputs are copied into the fallback graph's static buffer.
+GRAPHS_PER_MODEL = [int(_os.environ.get("SMPQ_GRAPHS", "4"))]
+
+
+def _capture(model, x_in, cal):
+    g = torch.cuda.CUDAGraph()
+    ctx = Ctx(x_in.shape[0], x_in.device, ranges=cal[0], cache=cal[2])
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        ctx.overflow = torch.zeros(2, dtype=torch.int32, device=x_in.device)
+        y_static = _forward(model, x_in, ctx)
+        cal[3].check(ctx.overflow[1:])
+    stats["graph_captures"] += 1
+    return g, ctx, y_static
 
 
 def _graph_forward(model, x, cal):
-    """Static forward through a captured HIP graph; returns (logits, overflow flag tensor)."""
+    """Static forward through a captured HIP graph; returns (logits, overflow flag tensor). The
+    graph reads the input where it lies when its address has a graph of its own (captured on first
+    sight, up to GRAPHS_PER_MODEL addresses, dropped with the calibration); otherwise the input is
+    copied into the fallback graph's static buffer."""
     key = _graph_key(model, x, cal)
-    entry = getattr(model, "_smpq_graph", None)
-    if entry is None or entry[0] != key:
-        model._smpq_graph = None
+    per_ptr = getattr(model, "_smpq_graphs", None)
+    if per_ptr is None or per_ptr.get("key") != key:
+        per_ptr = model._smpq_graphs = {"key": key}
+    hit = per_ptr.get((key, x.data_ptr()))
+    if hit is not None:
+        g, ctx, y_static = hit
+        g.replay()
+        stats["graph_replays"] += 1
+        return y_static.clone(), ctx.overflow
+    if len(per_ptr) - 1 < GRAPHS_PER_MODEL[0] and x.is_contiguous():
         y, ovf = _static_eager(model, x, cal)  # warm every cache outside the capture
         if any(ovf.tolist()):
             return y, ovf
+        g, ctx, y_static = _capture(model, x, cal)
+        per_ptr[(key, x.data_ptr())] = (g, ctx, y_static)
+        return y, ovf
+    entry = getattr(model, "_smpq_graph", None)
+    if entry is None or entry[0] != key:
+        model._smpq_graph = None
+        y, ovf = _static_eager(model, x, cal)
+        if any(ovf.tolist()):
+            return y, ovf
         static_x = x.clone()
-        g = torch.cuda.CUDAGraph()
-        ctx = Ctx(x.shape[0], x.device, ranges=cal[0], cache=cal[2])
-        torch.cuda.synchronize()
-        with torch.cuda.graph(g):
-            ctx.overflow = torch.zeros(2, dtype=torch.int32, device=x.device)
-            y_static = _forward(model, static_x, ctx)
-            cal[3].check(ctx.overflow[1:])
+        g, ctx, y_static = _capture(model, static_x, cal)
         model._smpq_graph = (key, g, static_x, ctx, y_static)
-        stats["graph_captures"] += 1
         return y, ovf
     _, g, static_x, ctx, y_static = entry
-    if x.data_ptr() != static_x.data_ptr():
-        static_x.copy_(x)
+    static_x.copy_(x)
     g.replay()
     stats["graph_replays"] += 1
     return y_static.clone(), ctx.overflow

@@ -168,7 +168,7 @@ class ResNet(nn.Module):
     def _apply(self, fn, *args, **kwargs):
         # .to() / .cuda() / .half() replace buffer tensors: drop the engine's cached references
         # (signature tensor list, captured graph) so they are rebuilt from the new tensors
-        for k in ("_smpq_graph", "_smpq_dyn", "_smpq_ranges"):
+        for k in ("_smpq_graph", "_smpq_graphs", "_smpq_dyn", "_smpq_ranges", "_smpq_fp"):
             self.__dict__.pop(k, None)
         return super()._apply(fn, *args, **kwargs)
 

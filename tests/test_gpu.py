@@ -893,21 +893,35 @@ def test_chunked_forward_identical(gpu, mode):
 
 
 def test_graph_replay_matches_eager(gpu):
+    """Graph replay == eager, bitwise: graphs captured on the inputs' own memory (one per input
+    address, no input copy) and the fallback graph that copies its input into a static buffer."""
     from smpq import engine, stats
     net = build_model(gpu, "resnet50", "r50_mixed")
     x = torch.randn(6, 3, 224, 224, generator=torch.Generator().manual_seed(14)).to(gpu)
     x2 = torch.randn(6, 3, 224, 224, generator=torch.Generator().manual_seed(15)).to(gpu)
-    with torch.no_grad():
-        engine.USE_GRAPH[0] = False
-        net(x)  # calibrate
-        e1, e2 = net(x), net(x2)
-        engine.USE_GRAPH[0] = True
-        c0, r0 = stats["graph_captures"], stats["graph_replays"]
-        g1 = net(x)   # capture
-        g2 = net(x2)  # replay with new input
-        g3 = net(x)   # replay
-    assert stats["graph_captures"] == c0 + 1 and stats["graph_replays"] == r0 + 2
-    assert torch.equal(g1, e1) and torch.equal(g2, e2) and torch.equal(g3, e1)
+    old = engine.GRAPHS_PER_MODEL[0]
+    try:
+        with torch.no_grad():
+            engine.USE_GRAPH[0] = False
+            net(x)  # calibrate
+            e1, e2 = net(x), net(x2)
+            engine.USE_GRAPH[0] = True
+            c0, r0 = stats["graph_captures"], stats["graph_replays"]
+            g1 = net(x)   # capture on x's memory
+            g2 = net(x2)  # capture on x2's memory
+            g3 = net(x)   # replay (x's graph)
+            g4 = net(x2)  # replay (x2's graph)
+            x.copy_(x2)
+            g5 = net(x)   # replay of x's graph on new content at the same address
+            assert stats["graph_captures"] == c0 + 2 and stats["graph_replays"] == r0 + 3
+            engine.GRAPHS_PER_MODEL[0] = 0  # fallback: one graph, inputs copied in
+            net._smpq_graphs = None
+            f1, f2, f3 = net(x2), net(x2.clone()), net(x2.clone())
+            assert stats["graph_captures"] == c0 + 3 and stats["graph_replays"] == r0 + 5
+    finally:
+        engine.GRAPHS_PER_MODEL[0] = old
+    assert torch.equal(g1, e1) and torch.equal(g2, e2) and torch.equal(g3, e1) and torch.equal(g4, e2)
+    assert torch.equal(g5, e2) and torch.equal(f1, e2) and torch.equal(f2, e2) and torch.equal(f3, e2)
 
 
 def test_graph_fast_path_never_returns_stale_weights(gpu):

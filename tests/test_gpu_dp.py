@@ -128,3 +128,4 @@ def test_static_forward_refuses_caller_capture(gpu, monkeypatch):
             net(x)
         monkeypatch.undo()
         np.testing.assert_array_equal(net(x).shape, (2, 1000))
+
