@@ -1,0 +1,94 @@
+"""One semilayer step of the reference's search drivers, replayed through the drop-in modules on
+the GPU (resnet50_main.py:176-243; resnet18_main.py / resnet34_main.py run the same loop):
+
+  quantize a semilayer channel by channel with ``conv.weight.data =
+  functions.channel_wise_quantizationperchan(conv.weight.data, w_bit, cnum)`` (:189-197), then
+  ``acc, loss, afteroutputs = functions.evaluate_acc_loss_softmax(net, device, val_loader)`` and
+  ``functions.KLdiv(originaloutputs, afteroutputs)`` (:204-205); on ``acc >= preacc``
+  ``torch.save(net.state_dict(), pthname)`` (:212), otherwise ``net.load_state_dict(torch.load(
+  pthname))`` and a re-evaluation (:233-236).
+
+Checked against the oracle (the reference's CPU forward on the same fake-quantized weights,
+oracle/torch_ref.py, and functions.py:84-149 restated in oracle/eval_ref.py) on the same images:
+top-1 accuracy exact, loss within 1e-3 relative, KL within 1 % relative (the KL of a semilayer
+step is a difference of two nearby softmaxes, so the 2e-4 logit tolerance of DESIGN.md 1 shows
+up amplified in it). The rejected step's restore must give the accepted step's evaluation back
+bit for bit (every cache — packed codes, folded BN, static ranges, graphs — follows
+``load_state_dict``)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from test_gpu import build_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_eval(arch, net, loader):
+    from oracle import eval_ref, torch_ref
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items() if not k.endswith(("qbits", "qstep"))}
+    batches = [(torch_ref.resnet_forward(arch, sd, x).numpy(), y.numpy()) for x, y in loader]
+    return eval_ref.evaluate_acc_loss_softmax(batches)
+
+
+def _quantize_semilayer(conv, w_bit, channels):
+    import functions
+    for cnum in channels:  # resnet50_main.py:189-197, one channel per call
+        conv.weight.data = functions.channel_wise_quantizationperchan(conv.weight.data, w_bit, cnum)
+
+
+@pytest.mark.parametrize("mode", ["static", "dynamic"])
+def test_semilayer_step_through_dropin(gpu, tmp_path, monkeypatch, mode):
+    import functions
+    from oracle import eval_ref
+    from smpq import engine
+    monkeypatch.setenv("SMPQ_SYNTHETIC", "1")
+    import imagenet
+    arch = "resnet18"
+    net = build_model(gpu, arch, None, "r18_u8_cal")  # BN-recalibrated parity model, fp32 weights
+    loader = list(imagenet.SyntheticImageNet(n_images=32, batch_size=16, seed=5))
+    # labels the network gets mostly right, so that the accuracy moves with the quantization
+    from oracle import torch_ref
+    sd0 = {k: v.detach().cpu() for k, v in net.state_dict().items() if not k.endswith(("qbits", "qstep"))}
+    loader = [(x, torch.where(torch.arange(len(y)) % 4 == 0, y, torch_ref.resnet_forward(arch, sd0, x).argmax(1)))
+              for x, y in loader]
+    old_mode = engine.get_range_mode()
+    engine.set_range_mode(mode)
+    try:
+        preacc, preloss, originaloutputs = functions.evaluate_acc_loss_softmax(net, gpu, loader)
+        r_acc, r_loss, r_orig = _oracle_eval(arch, net, loader)
+        assert preacc == r_acc and abs(preloss - r_loss) <= 1e-3 * abs(r_loss)
+
+        # semilayer 1: every channel of layer2.0.conv1 at 4 bits, accepted
+        conv = net.layer2[0].conv1
+        _quantize_semilayer(conv, 4, range(conv.out_channels))
+        assert conv.fully_quantized()
+        acc, loss, afteroutputs = functions.evaluate_acc_loss_softmax(net, gpu, loader)
+        kldiv = functions.KLdiv(originaloutputs, afteroutputs)
+        r_acc, r_loss, r_after = _oracle_eval(arch, net, loader)
+        r_kl = eval_ref.kldiv(r_orig, r_after)
+        print("%s step 1: acc %.4f (oracle %.4f) loss %.6f (oracle %.6f) KL %.4e (oracle %.4e)"
+              % (mode, acc, r_acc, loss, r_loss, kldiv, r_kl))
+        assert acc == r_acc
+        assert abs(loss - r_loss) <= 1e-3 * abs(r_loss)
+        assert abs(kldiv - r_kl) <= 0.01 * r_kl
+        pth = os.path.join(tmp_path, "step.pth")
+        torch.save(net.state_dict(), pth)  # resnet50_main.py:212 (acc >= preacc branch)
+        accepted = (acc, loss, [o.clone() for o in afteroutputs])
+
+        # semilayer 2: the first half of layer3.1.conv2 at 4 bits, then rejected and restored
+        conv2 = net.layer3[1].conv2
+        _quantize_semilayer(conv2, 4, range(conv2.out_channels // 2))
+        acc2, loss2, out2 = functions.evaluate_acc_loss_softmax(net, gpu, loader)
+        r_acc2, r_loss2, r_out2 = _oracle_eval(arch, net, loader)
+        assert acc2 == r_acc2 and abs(loss2 - r_loss2) <= 1e-3 * abs(r_loss2)
+        net.load_state_dict(torch.load(pth, weights_only=True))  # resnet50_main.py:233-234
+        assert not conv2.fully_quantized() and conv2._bits_host.max() == 0  # metadata restored too
+        debugacc, debugloss, debugoutputs = functions.evaluate_acc_loss_softmax(net, gpu, loader)  # :236
+        assert debugacc == accepted[0] and debugloss == accepted[1]
+        for a, b in zip(debugoutputs, accepted[2]):
+            assert torch.equal(a, b)
+    finally:
+        engine.set_range_mode(old_mode)
