@@ -40,6 +40,21 @@ constexpr int kAblate = SMPQ_DIAG_ABLATE;
 
 }  // namespace
 
+// Diagnostic builds only (tools/stamp_bench.hip, -DSMPQ_STAMPS): lane 0 of every wave records the
+// shader clock (s_memtime) at fixed points of the block's life into smpq_stamps (32 slots per
+// wave, vector stores); the product library never defines SMPQ_STAMPS.
+#ifdef SMPQ_STAMPS
+__device__ unsigned long long* smpq_stamps;
+#define SMPQ_STAMP(slot)                                                                                \
+  do {                                                                                                  \
+    if (lane == 0) smpq_stamps[((size_t)bid * NW + wave) * 32 + (slot)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define SMPQ_STAMP(slot) \
+  do {                   \
+  } while (0)
+#endif
+
 // S2D: the space-to-depth stem. The image is stored as 16-channel pixels ([2x2 block][4 ch]) and
 // the 7x7/2 conv is a 4x4/1 conv over them (pad 2, zero taps where the 8x8 extension falls
 // outside 7x7); a 64-B K step is one tap row: lane chunk c = the 16 channels of tap column c.
@@ -83,6 +98,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  SMPQ_STAMP(0);
   __builtin_assume(wave >= 0 && wave < NW);
   const int wc = wave / WAVES_P, wp = wave % WAVES_P;
 
@@ -421,6 +437,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 #pragma unroll
     for (int st = 0; st < NST - 1; ++st)
       if (st < nsteps) issue_next();
+    SMPQ_STAMP(1);
     for (int ks = 0; ks < nsteps; ++ks) {
       // this wave's DMA of step ks has landed (the younger steps' may still fly) and its reads of
       // step ks-1 are done; after the barrier every wave's are, so stage ks is readable and the
@@ -433,14 +450,30 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      if (ks < 16) SMPQ_STAMP(2 + ks);
       const int8_t* sb = lds + rbuf * STAGE;
       rbuf = rbuf + 1 == NST ? 0 : rbuf + 1;
       // fragments of MFMA K step h of this stage (the DMA below writes the other stage, so the
       // second half may be read after the first half's MFMAs: half the fragment registers live)
       Frags f;
       read_frags(f, sb, 0);
+#ifdef SMPQ_STAMPS
+      if (ks == 6) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        SMPQ_STAMP(18);
+      }
+#endif
       issue_next();  // the DMA of step ks + NST - 1 into the stage step ks - 1 used
+      if (ks == 6) SMPQ_STAMP(19);
       mma(f);
+#ifdef SMPQ_STAMPS
+      if (ks == 6) {
+        int keep = acc[0][0][0].x;
+        asm volatile("v_mov_b32 %0, %0" : "+v"(keep));  // after the MFMAs have retired
+        SMPQ_STAMP(20);
+        acc[0][0][0].x = keep;
+      }
+#endif
 #pragma unroll
       for (int h = 1; h < KH; ++h) {
         read_frags(f, sb, h);
@@ -449,6 +482,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     }
   }
 
+  SMPQ_STAMP(21);
   if constexpr ((kAblate & 16) != 0) {  // diagnostic: no epilogue at all (keep the MFMAs live)
     int keep = 0;
 #pragma unroll
@@ -741,6 +775,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     const bool ovf = LEAN ? vmax > qmax : rintf(__fmul_rn(vmax, a.yq_inv)) > qmax;
     if (__any(ovf) && lane == 0) atomicMax(a.overflow, 1);
   }
+  SMPQ_STAMP(22);
 }
 
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,

@@ -1,0 +1,124 @@
+// Where does a K step of the LDS-DMA conv kernel spend its cycles? Diagnostic harness: compiles ONE
+// qconv_glds_kernel instance with -DSMPQ_STAMPS (shader-clock stamps at fixed points, see
+// conv_glds.hip) and runs it on a synthetic R50 shape (operand values random: timing only).
+//
+// hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DSMPQ_STAMPS -DSMPQ_KERNEL_ONLY \
+//   -I semilayer-wise-mixed-precision-quantization_amd/csrc tools/stamp_bench.hip -o tools/bin/stamp_bench
+// ./tools/bin/stamp_bench [cin cout k hw [bk]]   (default: 3x3 256->256 at 14x14, B = 256, BK 64)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "conv_glds.hip"
+
+using namespace smpq;
+
+#define CK(x)                                                         \
+  do {                                                                \
+    hipError_t e_ = (x);                                              \
+    if (e_ != hipSuccess) {                                           \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));          \
+      return 1;                                                       \
+    }                                                                 \
+  } while (0)
+
+template <int BK>
+int run(int argc, char** argv) {
+  const int n = 256, cin = argc > 1 ? atoi(argv[1]) : 256, cout = argc > 2 ? atoi(argv[2]) : 256,
+            k = argc > 3 ? atoi(argv[3]) : 3, hw = argc > 4 ? atoi(argv[4]) : 14;
+  constexpr int L = 3, LW = 1, WAVES_C = 2, WAVES_P = 2, WC = 4, WP = 2, NST = 2, NW = 4;
+  constexpr int BC = 16 * WC * WAVES_C, BP = 16 * WP * WAVES_P, STAGE = (LW * BC + L * BP) * BK;
+  ConvArgs a{};
+  a.n = n; a.h = hw; a.w = hw; a.cin = cin; a.cout = cout; a.kh = k; a.kw = k; a.stride = 1; a.pad = k / 2;
+  a.ho = hw; a.wo = hw; a.M = n * hw * hw; a.K = k * k * cin; a.cchunks = cin / 64; a.ksteps = k * k * a.cchunks;
+  a.plane = (long long)n * hw * hw * cin; a.wplane = (long long)cout * a.K;
+  a.relu = 1; a.inv_qmax = 1.f / 8323072.f; a.yq_inv = 8323072.f / 1000.f;
+  fast_div_init(a.ho * a.wo, a.hw_mul, a.hw_shr);
+  fast_div_init(a.wo, a.wo_mul, a.wo_shr);
+  const int mt = (a.M + BP - 1) / BP, nt = (cout + BC - 1) / BC, blocks = mt * nt;
+  fast_div_init(nt, a.ntc_mul, a.ntc_shr);
+  int8_t *xq, *codes, *yq;
+  float *amax, *cs, *sh;
+  int32_t* ovf;
+  unsigned long long* st;
+  CK(hipMalloc(&xq, L * a.plane));
+  CK(hipMalloc(&codes, a.wplane));
+  CK(hipMalloc(&yq, (size_t)L * a.M * cout));
+  CK(hipMalloc(&amax, n * 4));
+  CK(hipMalloc(&cs, cout * 4));
+  CK(hipMalloc(&sh, cout * 4));
+  CK(hipMalloc(&ovf, 4));
+  CK(hipMalloc(&st, (size_t)blocks * NW * 32 * 8));
+  {
+    std::vector<int8_t> hx(L * a.plane), hw8(a.wplane);
+    for (auto& v : hx) v = (int8_t)(rand() % 256 - 128);
+    for (auto& v : hw8) v = (int8_t)(rand() % 64 - 32);
+    std::vector<float> one(std::max(n, cout), 1e-3f);
+    CK(hipMemcpy(xq, hx.data(), hx.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(codes, hw8.data(), hw8.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(amax, one.data(), n * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(cs, one.data(), cout * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(sh, 0, cout * 4));
+    CK(hipMemset(ovf, 0, 4));
+    CK(hipMemset(st, 0, (size_t)blocks * NW * 32 * 8));
+  }
+  a.xq = xq; a.x_absmax = amax; a.codes = codes; a.col_scale = cs; a.col_shift = sh; a.yq = yq; a.overflow = ovf;
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(smpq_stamps), &st, sizeof(st)));
+  auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, 2, false, NST, BK, true, false>;
+  const int nsteps = a.ksteps / (BK / 64);
+  const int lds = std::min(nsteps, NST) * STAGE;
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * NW), lds, 0, a);
+  CK(hipEventRecord(e0));
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * NW), lds, 0, a);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  std::vector<unsigned long long> h((size_t)blocks * NW * 32);
+  CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+  // per wave: prologue (0->1), per K step (barrier to barrier, steps 1..14), step 6 split
+  // (barrier -> fragments in registers -> DMA issued -> MFMAs retired -> next barrier), K loop end
+  // -> epilogue end; medians over all waves
+  auto med = [](std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    return v.empty() ? 0.0 : v[v.size() / 2];
+  };
+  std::vector<double> pro, step, rd, iss, mf, rest, epi, life, skew;
+  for (int b = 0; b < blocks; ++b) {
+    unsigned long long bar6[NW];
+    for (int w = 0; w < NW; ++w) {
+      const unsigned long long* t = &h[((size_t)b * NW + w) * 32];
+      pro.push_back((double)(t[1] - t[0]));
+      const int last = std::min(nsteps, 16) - 1;
+      if (last >= 2) step.push_back((double)(t[2 + last] - t[3]) / (last - 1));
+      if (nsteps > 7) {
+        rd.push_back((double)(t[18] - t[8]));
+        iss.push_back((double)(t[19] - t[18]));
+        mf.push_back((double)(t[20] - t[19]));
+        rest.push_back((double)(t[9] - t[20]));
+      }
+      epi.push_back((double)(t[22] - t[21]));
+      life.push_back((double)(t[22] - t[0]));
+      bar6[w] = t[8];
+    }
+    unsigned long long lo = bar6[0], hi = bar6[0];
+    for (int w = 1; w < NW; ++w) lo = std::min(lo, bar6[w]), hi = std::max(hi, bar6[w]);
+    skew.push_back((double)(hi - lo));
+  }
+  printf("{\"shape\": \"%dx%d %d->%d at %d^2, B=%d, BK=%d\", \"blocks\": %d, \"ksteps\": %d, \"kernel_us\": %.1f, "
+         "\"median_cycles\": {\"prologue\": %.0f, \"per_k_step\": %.0f, \"step6_barrier_to_frags\": %.0f, "
+         "\"step6_dma_issue\": %.0f, \"step6_mfma_issue_to_retire\": %.0f, \"step6_to_next_barrier\": %.0f, "
+         "\"epilogue\": %.0f, \"block_life\": %.0f, \"barrier_exit_skew\": %.0f}}\n",
+         k, k, cin, cout, hw, n, BK, blocks, nsteps, ms * 1e3, med(pro), med(step), med(rd), med(iss), med(mf),
+         med(rest), med(epi), med(life), med(skew));
+  return 0;
+}
+
+int main(int argc, char** argv) { return (argc > 5 && atoi(argv[5]) == 128) ? run<128>(argc, argv) : run<64>(argc, argv); }
