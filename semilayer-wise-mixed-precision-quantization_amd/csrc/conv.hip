@@ -31,6 +31,7 @@
 // output tile so residual loads and output stores are whole 16-B pieces of contiguous rows.
 #include <algorithm>
 #include <climits>
+#include <cstdint>
 #include <cstdlib>
 #include <string>
 
@@ -944,13 +945,13 @@ static int conv_args_q(const int8_t* xq, const float* x_absmax, int n, int h, in
   return SMPQ_OK;
 }
 
-extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
-                                 const int8_t* codes, int wlimbs, const int32_t* offset, int cout, int kh,
-                                 int kw, int stride, int pad, const float* col_scale,
-                                 const float* col_shift, const float* residual, int relu, int limbs,
-                                 float* y, float* y_absmax, int8_t* yq, float yq_range, int32_t* overflow,
-                                 const int8_t* residual_q, float residual_range, int tile_cfg,
-                                 smpq_stream_t stream) {
+extern "C" int smpq_conv2d_fwd_q_km(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+                                    const int8_t* codes, const int8_t* codes_kmajor, int wlimbs,
+                                    const int32_t* offset, int cout, int kh, int kw, int stride, int pad,
+                                    const float* col_scale, const float* col_shift, const float* residual, int relu,
+                                    int limbs, float* y, float* y_absmax, int8_t* yq, float yq_range,
+                                    int32_t* overflow, const int8_t* residual_q, float residual_range, int tile_cfg,
+                                    smpq_stream_t stream) {
   ConvArgs a;
   const int rc = conv_args_q(xq, x_absmax, n, h, w, cin, codes, wlimbs, offset, cout, kh, kw, stride, pad, col_scale,
                              col_shift, residual, relu, limbs, y, y_absmax, yq, yq_range, overflow, residual_q,
@@ -974,10 +975,53 @@ extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n,
   if (tile_cfg >= kNumTileCfgs + glds_num_cfgs()) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   if (tile_cfg >= kNumTileCfgs) {
     if (smallc) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: LDS-DMA tile configs need cin % 64 == 0");
+    if (codes_kmajor) {  // the same codes, K-major (smpq_weights_kmajor): whole-line weight DMA pieces
+      a.codes = codes_kmajor;
+      a.w_kmajor = 1;
+    }
     return launch_glds(tile_cfg - kNumTileCfgs, limbs, wlimbs, a, s);
   }
   if (tile_cfg >= kNumBaseCfgs) return dispatch_limbs<1>(tile_cfg - kNumBaseCfgs, smallc, limbs, wlimbs, a, s);
   return dispatch_limbs<2>(tile_cfg, smallc, limbs, wlimbs, a, s);
+}
+
+extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+                                 const int8_t* codes, int wlimbs, const int32_t* offset, int cout, int kh,
+                                 int kw, int stride, int pad, const float* col_scale,
+                                 const float* col_shift, const float* residual, int relu, int limbs,
+                                 float* y, float* y_absmax, int8_t* yq, float yq_range, int32_t* overflow,
+                                 const int8_t* residual_q, float residual_range, int tile_cfg,
+                                 smpq_stream_t stream) {
+  return smpq_conv2d_fwd_q_km(xq, x_absmax, n, h, w, cin, codes, nullptr, wlimbs, offset, cout, kh, kw, stride, pad,
+                              col_scale, col_shift, residual, relu, limbs, y, y_absmax, yq, yq_range, overflow,
+                              residual_q, residual_range, tile_cfg, stream);
+}
+
+namespace {
+// [LW][cout][K] -> [LW][K/64][cout][64], one 16-B chunk per thread
+__global__ void weights_kmajor_kernel(const int4* __restrict__ src, int4* __restrict__ dst, int cout, int kc,
+                                      long long chunks_per_limb, long long total) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const long long lw = i / chunks_per_limb, r = i - lw * chunks_per_limb;
+  const int q = (int)(r & 3);            // 16-B chunk in the 64-B slice
+  const long long t = r >> 2;            // (row, slice) in the source order
+  const int row = (int)(t / kc), sl = (int)(t - (long long)row * kc);
+  dst[lw * chunks_per_limb + ((long long)sl * cout + row) * 4 + q] = src[i];
+}
+}  // namespace
+
+extern "C" int smpq_weights_kmajor(const int8_t* codes, int wlimbs, int cout, int K, int8_t* out,
+                                   smpq_stream_t stream) {
+  if (!codes || !out) return fail(SMPQ_E_INVALID, "smpq_weights_kmajor: null pointer");
+  if (wlimbs < 1 || wlimbs > 3 || cout <= 0 || K <= 0 || K % 64 != 0)
+    return fail(SMPQ_E_SHAPE, "smpq_weights_kmajor: need 1..3 limbs, cout > 0, K % 64 == 0");
+  if (((uintptr_t)codes | (uintptr_t)out) & 15) return fail(SMPQ_E_INVALID, "smpq_weights_kmajor: 16-B alignment");
+  const long long per = (long long)cout * K / 16, total = per * wlimbs;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(weights_kmajor_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const int4*>(codes), reinterpret_cast<int4*>(out), cout, K / 64, per, total);
+  return check_hip(hipGetLastError(), "weights_kmajor_kernel launch");
 }
 
 extern "C" int smpq_conv2d_fwd_ex(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,

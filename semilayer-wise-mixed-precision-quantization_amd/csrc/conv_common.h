@@ -35,6 +35,10 @@ struct ConvArgs {
   int hw_shr, wo_shr, ntc_shr;
   float inv_qmax;
   int s2d;  // space-to-depth stem (smpq_stem_conv_s2d_q): cin 16, 4 x 4 taps, K step = one tap row
+  // codes in the K-major layout [LW][K/64][cout][64] (smpq_conv2d_fwd_q_km; LDS-DMA kernel only):
+  // the 64-B K slices of 16 consecutive output channels are one contiguous KiB, so every weight
+  // DMA piece is whole cache lines instead of 16 half lines
+  int w_kmajor;
 };
 
 // Division by a runtime constant d >= 1 for numerators in [0, 2^31): p = 31 + ceil(log2 d),

@@ -127,9 +127,12 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     const int p = wave + NW * s;  // weight piece: limb p / (BC/RPP), rows RPP * (p % (BC/RPP)) + ...
     const int lw = p / (BC / RPP), bi = p % (BC / RPP);
     const int row = n0 + RPP * bi + prow;
-    wsrc[s] = (p < WPIECES && row < a.cout)
-                  ? (unsigned)((long long)lw * a.wplane + (long long)row * a.K + 16 * pchunk_of(bi))
-                  : kOOB;
+    // logical 16-B chunk lc of the row's BK-wide K slice: row-major [LW][cout][K] at row * K + 16 lc;
+    // K-major [LW][K/64][cout][64] at (lc / 4) 64-B slices of cout rows further, row * 64 + 16 (lc % 4)
+    const int lc = pchunk_of(bi);
+    const long long woff = a.w_kmajor ? (long long)(lc >> 2) * a.cout * 64 + (long long)row * 64 + 16 * (lc & 3)
+                                      : (long long)row * a.K + 16 * lc;
+    wsrc[s] = (p < WPIECES && row < a.cout) ? (unsigned)((long long)lw * a.wplane + woff) : kOOB;
   }
   int apix[ASLOTS], aih[ASLOTS], aiw[ASLOTS];
 #pragma unroll
@@ -161,12 +164,15 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
 
   // K position of step ks: tap (kr, kc), channel chunk c0 (scalar, advanced incrementally)
+  // bytes between the weight slices of consecutive K steps (row-major: BK along the row; K-major:
+  // BK / 64 slices of cout rows)
+  const unsigned wstep = __builtin_amdgcn_readfirstlane(a.w_kmajor ? (unsigned)(BK * a.cout) : (unsigned)BK);
   auto issue = [&](int buf, int kr, int kc, int c0, int ks) {
     const unsigned sb = lds0 + buf * STAGE;
 #pragma unroll
     for (int s = 0; s < WSLOTS; ++s) {
       const int p = wave + NW * s;
-      if (p < WPIECES && !(kAblate & 4)) dma16(sb + p * 1024, wrs, wsrc[s], __builtin_amdgcn_readfirstlane(ks * BK));
+      if (p < WPIECES && !(kAblate & 4)) dma16(sb + p * 1024, wrs, wsrc[s], __builtin_amdgcn_readfirstlane(ks * wstep));
     }
     const int tapoff = (kr * a.w + kc) * a.cin + c0;
 #pragma unroll

@@ -138,7 +138,30 @@ def pack_weights_ex(w, step, wlimbs):
         _lib.check(lib.smpq_pack_weights_ex(_lib.ptr(w), cout, cin, kh, kw, _lib.ptr(step), int(wlimbs),
                                             _lib.ptr(codes), _lib.ptr(offset), _lib.ptr(wscale), _lib.ptr(status),
                                             _lib.stream_ptr()), "smpq_pack_weights_ex")
+    if KMAJOR[0] and cin % 64 == 0:
+        # the K-major copy the LDS-DMA tiles stage their weight pieces from (whole cache lines);
+        # it lives and dies with these codes
+        codes._smpq_km = weights_kmajor(codes)
     return codes, offset, wscale, status
+
+
+KMAJOR = [os.environ.get("SMPQ_KMAJOR", "1") != "0"]
+
+
+def weights_kmajor(codes):
+    """codes int8 [LW, cout, K] (K % 64 == 0) -> the K-major copy [LW, K/64, cout, 64]
+    (smpq_weights_kmajor) that smpq_conv2d_fwd_q_km's LDS-DMA tiles read."""
+    if codes.dim() == 2:
+        codes = codes.unsqueeze(0)
+    wl, cout, K = codes.shape
+    _req(codes.is_cuda and codes.dtype == torch.int8 and codes.is_contiguous() and K % 64 == 0,
+         "weights_kmajor: need contiguous int8 [LW, cout, K] with K % 64 == 0")
+    out = torch.empty(wl, K // 64, cout, 64, dtype=torch.int8, device=codes.device)
+    lib = _lib.load()
+    with torch.cuda.device(codes.device):
+        _lib.check(lib.smpq_weights_kmajor(_lib.ptr(codes), int(wl), int(cout), int(K), _lib.ptr(out),
+                                           _lib.stream_ptr()), "smpq_weights_kmajor")
+    return out
 
 
 def image_quantize(x, x_absmax, limbs=None):
@@ -384,17 +407,21 @@ def tile_kind(cfg):
 
 def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
              residual=None, relu=False, y_absmax=None, out=None, tile_cfg=-1,
-             emit_range=None, overflow=None, want_f32=True, residual_q=None, residual_range=None):
+             emit_range=None, overflow=None, want_f32=True, residual_q=None, residual_range=None,
+             weight_layout="auto"):
     """Quantized conv on int8 limb planes xq [L, n, h, w, cin] (from act_quantize / image_quantize /
     maxpool_quantize / a previous conv2d_q) and weight limb planes codes [LW, cout, K] (or
     [cout, K] for LW = 1): y = conv(x, w) * s_x * col_scale + col_shift (+res) (relu), NHWC fp32.
     With ``emit_range`` (static range of the output, float) the epilogue also writes the output's
     int8 limb planes [L, n, ho, wo, cout] and sets ``overflow`` (int32 [1]) if a value exceeded the
     range; returns (y or None, yq) then. ``residual_q`` (+ ``residual_range``): the residual as
-    int8 limb planes [L, n, ho, wo, cout] instead of fp32 ``residual``."""
+    int8 limb planes [L, n, ho, wo, cout] instead of fp32 ``residual``. ``weight_layout``: "auto"
+    lets the LDS-DMA tiles read the K-major copy pack_weights_ex attached to ``codes``
+    (bitwise the same results), "rowmajor" keeps them on ``codes`` itself."""
     _req(xq.is_cuda and xq.dtype == torch.int8 and xq.dim() == 5 and xq.is_contiguous(), "conv: xq must be [L,n,h,w,c] int8")
     limbs, n, h, w, cin = xq.shape
     _req(limbs in (1, 2, 3), "conv: limbs")
+    km = getattr(codes, "_smpq_km", None) if weight_layout == "auto" else None
     if codes.dim() == 2:
         codes = codes.unsqueeze(0)
     wlimbs, cout, K = codes.shape
@@ -435,12 +462,15 @@ def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_sh
     if hook is not None:
         hook.begin()
     with torch.cuda.device(xq.device):
-        _lib.check(lib.smpq_conv2d_fwd_q(
-            _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, cin, _lib.ptr(codes), int(wlimbs), _lib.ptr(offset), cout,
+        if km is not None:
+            _req(km.shape == (wlimbs, K // 64, cout, 64) and km.device == xq.device, "conv: K-major codes")
+        _lib.check(lib.smpq_conv2d_fwd_q_km(
+            _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, cin, _lib.ptr(codes), _lib.ptr(km), int(wlimbs),
+            _lib.ptr(offset), cout,
             kh, kw, stride, pad, _lib.ptr(col_scale), _lib.ptr(col_shift), _lib.ptr(residual), 1 if relu else 0,
             int(limbs), _lib.ptr(out), _lib.ptr(y_absmax), _lib.ptr(yq), float(emit_range or 0.0),
             _lib.ptr(overflow), _lib.ptr(residual_q), float(residual_range or 0.0), int(tile_cfg),
-            _lib.stream_ptr()), "smpq_conv2d_fwd_q")
+            _lib.stream_ptr()), "smpq_conv2d_fwd_q_km")
     if hook is not None:
         cin_real = 3 if cin == 4 else cin  # the 4-channel stem planes carry RGB + a zero channel
         hook.end(alg_work(n, h, w, cin_real, cout, kh, kw, ho, wo, limbs, wlimbs, out is not None, yq is not None,

@@ -987,6 +987,53 @@ def test_tile_configs_deterministic(gpu, shape):
             assert torch.equal(y, y0) and torch.equal(q, q0), (c, rep)
 
 
+@pytest.mark.parametrize("shape", [(128, 256, 3, 1, 14, 1), (256, 512, 1, 2, 28, 3), (512, 128, 1, 1, 14, 1),
+                                   (64, 64, 3, 1, 20, 1), (192, 80, 3, 1, 9, 1), (128, 112, 1, 1, 11, 3)],
+                         ids=lambda s: "c%d_o%d_k%d_s%d_h%d_lw%d" % s)
+def test_kmajor_weights_bitwise(gpu, shape):
+    """The K-major weight copy (smpq_weights_kmajor, round 3) is the permutation it claims, and
+    every LDS-DMA tile config reading it (smpq_conv2d_fwd_q_km) gives the row-major result bit for
+    bit — fp32 output, limb planes, limb-plane residual, overflow flag — incl. partial channel
+    tiles (cout % BC != 0), 128-B K steps and 24-bit fixed-point weights."""
+    from smpq import ops
+    cin, cout, k, s, h, wl = shape
+    limbs = 3
+    g = torch.Generator().manual_seed(cin * 7 + cout)
+    w = (torch.randn(cout, cin, k, k, generator=g) * 0.05).to(gpu)
+    if wl == 1:
+        step = ops.quantize_channels_(w.reshape(cout, -1), [6] * cout)
+        codes, offset, wscale, st = ops.pack_weights_ex(w, step, 1)
+        offset = offset if bool((offset != 0).any()) else None
+    else:
+        codes, _, wscale, st = ops.pack_weights_ex(w, None, wl)
+        offset = None
+    km = codes._smpq_km
+    K = codes.shape[-1]
+    assert torch.equal(km, codes.view(wl, cout, K // 64, 64).permute(0, 2, 1, 3).contiguous())
+    x = torch.relu(torch.randn(3, h, h, cin, generator=g)).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, limbs)
+    ho = (h + 2 * (k // 2) - k) // s + 1
+    rq = ops.act_quantize(torch.randn(3, ho, ho, cout, generator=g).clamp(-4, 4).to(gpu),
+                          torch.full((3,), 4.0, device=gpu), limbs)
+    shift = torch.linspace(-1, 1, cout, device=gpu)
+    kw = dict(residual_q=rq, residual_range=4.0, want_f32=True, relu=True)
+    ref = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, wscale, shift, weight_layout="rowmajor", **kw)
+    rng = float(ref.abs().max()) * 2.0
+    cfgs = [c for c in ops.tile_configs() if ops.tile_kind(c) in (ops.TILE_LDS_DMA, ops.TILE_LDS_DMA_K128)
+            and ops._tile_fits(c, limbs, wl, False, cout, cin, k)]
+    assert cfgs
+    for c in cfgs:
+        o0 = torch.zeros(1, dtype=torch.int32, device=gpu)
+        o1 = torch.zeros(1, dtype=torch.int32, device=gpu)
+        y0, q0 = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, wscale, shift, tile_cfg=c, emit_range=rng,
+                              overflow=o0, weight_layout="rowmajor", **kw)
+        y1, q1 = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, wscale, shift, tile_cfg=c, emit_range=rng,
+                              overflow=o1, **kw)
+        assert torch.equal(y0, y1) and torch.equal(q0, q1) and torch.equal(o0, o1), c
+        assert torch.equal(y0, ref), c
+
+
 def test_forward_independent_of_previous_input(gpu):
     """A forward's result must not depend on what ran before it (stale memory or registers): the
     static-range forward of x, then of x2, then of x again gives x's logits bit for bit, several

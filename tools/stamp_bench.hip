@@ -4,7 +4,9 @@
 //
 // hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DSMPQ_STAMPS -DSMPQ_KERNEL_ONLY \
 //   -I semilayer-wise-mixed-precision-quantization_amd/csrc tools/stamp_bench.hip -o tools/bin/stamp_bench
-// ./tools/bin/stamp_bench [cin cout k hw [bk]]   (default: 3x3 256->256 at 14x14, B = 256, BK 64)
+// ./tools/bin/stamp_bench [cin cout k hw [bk [stride]]]   (default: 3x3 256->256 at 14x14, B = 256, BK 64)
+// Without -DSMPQ_STAMPS it only times the launch (add -DSB_LW=3 for the downsample's weight limbs,
+// -DSMPQ_DIAG_ABLATE=N for conv_glds.hip's diagnostic ablations).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,12 +30,16 @@ using namespace smpq;
 template <int BK>
 int run(int argc, char** argv) {
   const int n = 256, cin = argc > 1 ? atoi(argv[1]) : 256, cout = argc > 2 ? atoi(argv[2]) : 256,
-            k = argc > 3 ? atoi(argv[3]) : 3, hw = argc > 4 ? atoi(argv[4]) : 14;
-  constexpr int L = 3, LW = 1, WAVES_C = 2, WAVES_P = 2, WC = 4, WP = 2, NST = 2, NW = 4;
+            k = argc > 3 ? atoi(argv[3]) : 3, hw = argc > 4 ? atoi(argv[4]) : 14,
+            stride = argc > 6 ? atoi(argv[6]) : 1;
+#ifndef SB_LW
+#define SB_LW 1
+#endif
+  constexpr int L = 3, LW = SB_LW, WAVES_C = 2, WAVES_P = 2, WC = 4, WP = 2, NST = 2, NW = 4;
   constexpr int BC = 16 * WC * WAVES_C, BP = 16 * WP * WAVES_P, STAGE = (LW * BC + L * BP) * BK;
   ConvArgs a{};
-  a.n = n; a.h = hw; a.w = hw; a.cin = cin; a.cout = cout; a.kh = k; a.kw = k; a.stride = 1; a.pad = k / 2;
-  a.ho = hw; a.wo = hw; a.M = n * hw * hw; a.K = k * k * cin; a.cchunks = cin / 64; a.ksteps = k * k * a.cchunks;
+  a.n = n; a.h = hw; a.w = hw; a.cin = cin; a.cout = cout; a.kh = k; a.kw = k; a.stride = stride; a.pad = k / 2;
+  a.ho = (hw + 2 * a.pad - k) / stride + 1; a.wo = a.ho; a.M = n * a.ho * a.wo; a.K = k * k * cin; a.cchunks = cin / 64; a.ksteps = k * k * a.cchunks;
   a.plane = (long long)n * hw * hw * cin; a.wplane = (long long)cout * a.K;
   a.relu = 1; a.inv_qmax = 1.f / 8323072.f; a.yq_inv = 8323072.f / 1000.f;
   fast_div_init(a.ho * a.wo, a.hw_mul, a.hw_shr);
@@ -45,7 +51,7 @@ int run(int argc, char** argv) {
   int32_t* ovf;
   unsigned long long* st;
   CK(hipMalloc(&xq, L * a.plane));
-  CK(hipMalloc(&codes, a.wplane));
+  CK(hipMalloc(&codes, LW * a.wplane));
   CK(hipMalloc(&yq, (size_t)L * a.M * cout));
   CK(hipMalloc(&amax, n * 4));
   CK(hipMalloc(&cs, cout * 4));
@@ -53,7 +59,7 @@ int run(int argc, char** argv) {
   CK(hipMalloc(&ovf, 4));
   CK(hipMalloc(&st, (size_t)blocks * NW * 32 * 8));
   {
-    std::vector<int8_t> hx(L * a.plane), hw8(a.wplane);
+    std::vector<int8_t> hx(L * a.plane), hw8(LW * a.wplane);
     for (auto& v : hx) v = (int8_t)(rand() % 256 - 128);
     for (auto& v : hw8) v = (int8_t)(rand() % 64 - 32);
     std::vector<float> one(std::max(n, cout), 1e-3f);
@@ -66,7 +72,12 @@ int run(int argc, char** argv) {
     CK(hipMemset(st, 0, (size_t)blocks * NW * 32 * 8));
   }
   a.xq = xq; a.x_absmax = amax; a.codes = codes; a.col_scale = cs; a.col_shift = sh; a.yq = yq; a.overflow = ovf;
+#ifdef SMPQ_STAMPS
   CK(hipMemcpyToSymbol(HIP_SYMBOL(smpq_stamps), &st, sizeof(st)));
+#else
+  printf("{\"shape\": \"%dx%d/%d %d->%d at %d^2, B=%d, BK=%d, LW=%d, ablate=%d\", \"kernel_us\": ", k, k, stride, cin, cout,
+         hw, n, BK, LW, SMPQ_DIAG_ABLATE);
+#endif
   auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, 2, false, NST, BK, true, false>;
   const int nsteps = a.ksteps / (BK / 64);
   const int lds = std::min(nsteps, NST) * STAGE;
@@ -76,11 +87,17 @@ int run(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * NW), lds, 0, a);
   CK(hipEventRecord(e0));
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * NW), lds, 0, a);
+  const int reps = 10;
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * NW), lds, 0, a);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms = 0;
   CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= reps;
+#ifndef SMPQ_STAMPS
+  printf("%.1f}\n", ms * 1e3);
+  return 0;
+#endif
   std::vector<unsigned long long> h((size_t)blocks * NW * 32);
   CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
   // per wave: prologue (0->1), per K step (barrier to barrier, steps 1..14), step 6 split
