@@ -568,7 +568,7 @@ def _static_eager(model, x, cal):
 
 def _graph_key(model, x, cal):
     return (tuple(x.shape), x.dtype, x.device, cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0],
-            CONCURRENT_DS[0], STREAMS[0])
+            CONCURRENT_DS[0], STREAMS[0], ops.KMAJOR[0])
 
 
 def _graph_ready(model, x, cal):
