@@ -15,7 +15,8 @@ pass quantizing the caller's net for its first semilayer before switching to fre
 """
 import torch
 
-from smpq import ops
+from smpq import engine, ops
+from smpq.models import ResNet
 from smpq.quant import channel_wise_quantizationperchan, quantize_wgt  # noqa: F401
 
 _SENTINEL = [0, 0, 100, 0, 0, 0, 0, 0]
@@ -32,6 +33,8 @@ def _run_eval(net, device, data_loader, want_probs):
         dev = torch.device("cuda", torch.cuda.current_device())
     stats = torch.zeros(4, dtype=torch.float64, device=dev)
     outputs = []
+    if isinstance(net, ResNet):
+        engine.new_evaluation(net)  # ranges from this pass's own first batch: history-independent
     with torch.no_grad():
         for x, y in data_loader:
             x = x.to(device, non_blocking=True)

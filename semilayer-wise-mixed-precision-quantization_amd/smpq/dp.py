@@ -70,10 +70,13 @@ def sharded_eval(net, loader, rank, world, device=None, keep_probs=True):
     kernel accumulates on its device, and one all-reduce of 4 doubles combines the ranks.
     Returns (acc, loss, this rank's softmax shards) — the shards stay where they were made and
     feed sharded_kldiv, so no logits or probabilities cross xGMI."""
-    from smpq import ops
+    from smpq import engine, ops
+    from smpq.models import ResNet
     dev = device or torch.device("cuda", torch.cuda.current_device())
     stats = torch.zeros(4, dtype=torch.float64, device=dev)
     probs = []
+    if isinstance(net, ResNet):
+        engine.new_evaluation(net)  # as functions.evaluate_acc_loss_softmax (history-independent)
     with torch.no_grad(), lockstep():
         for x, y in loader:
             s, e = shard_range(x.shape[0], rank, world)

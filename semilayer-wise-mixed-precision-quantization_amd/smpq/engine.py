@@ -536,7 +536,9 @@ def calibration_maxima(model, x, stale=False):
 def set_calibration(model, c, widen=True):
     """Install the static ranges range_l = HEADROOM * max_l of Calibration ``c``. With ``widen``
     and unchanged weights (same signature, same content as the previous calibration, e.g. an
-    overflow rerun) each range stays at least its previous value, so ranges only grow."""
+    overflow rerun) each range stays at least its previous value, so ranges only grow. Ranges
+    equal to the installed ones (same weights, same calibration batch) keep the installed
+    calibration object, and with it the graphs captured for it."""
     maxima = c.maxima.cpu().tolist()
     old = getattr(model, "_smpq_ranges", None)
     keep = widen and old is not None and not c.changed and old[1] == c.sig0
@@ -546,17 +548,31 @@ def set_calibration(model, c, widen=True):
         if keep and k in old[0]:
             r = max(r, old[0][k])
         ranges[k] = r
-    model._smpq_ranges = (ranges, _signature(model), {}, c.fp)
+    sig = _signature(model)
+    if old is not None and not c.changed and old[1] == sig and old[0] == ranges:
+        return
+    model._smpq_ranges = (ranges, sig, {}, c.fp)
 
 
-def calibrate(model, x, stale=False):
+def calibrate(model, x, stale=False, fresh=False):
     """Dynamic forward of ``x`` that (re)sets the per-layer static ranges; returns its logits.
-    In a data-parallel group the maxima are MAX-all-reduced over the ranks first."""
+    In a data-parallel group the maxima are MAX-all-reduced over the ranks first. ``fresh``: the
+    ranges come from this batch alone (no widening by earlier ranges: new_evaluation)."""
     c = calibration_maxima(model, x, stale)
     _dp_max_(c.maxima)
-    set_calibration(model, c)
+    set_calibration(model, c, widen=not fresh)
     stats["calibrations"] += 1
     return c.logits
+
+
+def new_evaluation(model):
+    """Start of an evaluation pass over a loader (functions.evaluate_acc_loss_softmax /
+    evaluate_loss, dp.sharded_eval): the next static-range forward recalibrates on its own batch,
+    so every evaluation's ranges are a function of the weights and of that evaluation's first
+    batch only — two evaluations of the same weights on the same loader give the same results
+    bit for bit, whatever ran before (an overflow rerun widens the ranges for the rest of the
+    pass only). Identical ranges keep the captured graphs."""
+    model._smpq_recal = True
 
 
 def _static_eager(model, x, cal):
@@ -666,17 +682,18 @@ def forward_fused(model, x):
         raise RuntimeError("smpq: the static-range forward cannot run inside a caller's graph capture "
                            "(it replays its own HIP graph); use dynamic range mode to capture it")
     cal = getattr(model, "_smpq_ranges", None)
+    fresh = model.__dict__.pop("_smpq_recal", False)
     if _DP[0] is not None:
         # collective decision: every rank calibrates, or none does
-        need = torch.tensor([0 if (cal is not None and cal[1] == _signature(model)) else 1], dtype=torch.int32,
-                            device=x.device)
+        need = torch.tensor([0 if (cal is not None and cal[1] == _signature(model) and not fresh) else 1],
+                            dtype=torch.int32, device=x.device)
         if int(_dp_max_(need).item()):
-            return calibrate(model, x)
+            return calibrate(model, x, fresh=fresh)
         y, ovf = _graph_forward(model, x, cal) if USE_GRAPH[0] else _static_eager(model, x, cal)
         _dp_max_(ovf)
     else:
-        if cal is None:
-            return calibrate(model, x)
+        if cal is None or fresh:
+            return calibrate(model, x, fresh=fresh)
         if USE_GRAPH[0] and _graph_ready(model, x, cal):
             # fast path: replay first, then validate on the host while the GPU runs; a changed
             # weight or BN buffer discards the result (recalibrate + recapture): nothing stale

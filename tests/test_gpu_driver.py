@@ -17,7 +17,6 @@ bit for bit (every cache — packed codes, folded BN, static ranges, graphs — 
 ``load_state_dict``)."""
 import os
 
-import numpy as np
 import pytest
 import torch
 
@@ -92,3 +91,28 @@ def test_semilayer_step_through_dropin(gpu, tmp_path, monkeypatch, mode):
             assert torch.equal(a, b)
     finally:
         engine.set_range_mode(old_mode)
+
+
+def test_evaluation_history_independent(gpu):
+    """Each evaluation pass calibrates its static ranges on its own first batch
+    (engine.new_evaluation): the same weights on the same loader give the same accuracy, loss and
+    softmax bit for bit whatever ran before — here a first pass whose second batch overflows (its
+    ranges widen) and a pass on a different loader in between."""
+    import functions
+    from smpq import engine, stats
+    net = build_model(gpu, "resnet18", "r18_u8", "r18_u8_cal")
+    g = torch.Generator().manual_seed(41)
+    xa = torch.randn(8, 3, 224, 224, generator=g)
+    ya = torch.randint(0, 1000, (8,), generator=g)
+    loader = [(xa, ya), (xa * 4.0, ya), (xa, ya)]  # the x4 batch exceeds ranges calibrated on xa
+    assert engine.get_range_mode() == "static"
+    o0 = stats["overflow_reruns"]
+    r1 = functions.evaluate_acc_loss_softmax(net, gpu, loader)
+    assert stats["overflow_reruns"] > o0
+    r2 = functions.evaluate_acc_loss_softmax(net, gpu, loader)
+    functions.evaluate_acc_loss_softmax(net, gpu, [(xa * 8.0, ya)])  # another history
+    r3 = functions.evaluate_acc_loss_softmax(net, gpu, loader)
+    for r in (r2, r3):
+        assert r[0] == r1[0] and r[1] == r1[1]
+        for a, b in zip(r[2], r1[2]):
+            assert torch.equal(a, b)

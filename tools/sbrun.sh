@@ -1,12 +1,9 @@
+#!/bin/bash
+# Timing-only runs of tools/stamp_bench.hip builds (tools/bin/sb_lw<LW>_a<ABLATE>), one line per shape.
+# usage: bash tools/sbrun.sh "<ablate values>"   (on the GPU box, from the repo root)
 set -e
-for b in sb_lw1_a0 sb_lw1_a64; do
-  timeout -k 10 60 ./tools/bin/$b 256 256 3 14 64 1
-  timeout -k 10 60 ./tools/bin/$b 1024 256 1 14 64 1
-  timeout -k 10 60 ./tools/bin/$b 128 128 3 28 64 1
-  timeout -k 10 60 ./tools/bin/$b 256 64 1 56 64 1
-done
-for b in sb_lw3_a0 sb_lw3_a64; do
-  timeout -k 10 60 ./tools/bin/$b 1024 2048 1 14 64 2
-  timeout -k 10 60 ./tools/bin/$b 512 1024 1 28 64 2
-  timeout -k 10 60 ./tools/bin/$b 256 512 1 56 64 2
+for a in ${1:-0}; do
+  for s in "256 256 3 14 64 1" "1024 256 1 14 64 1" "128 128 3 28 64 1" "512 512 3 7 64 1" "256 64 1 56 64 1"; do
+    timeout -k 10 60 ./tools/bin/sb_lw1_a$a $s
+  done
 done
