@@ -8,8 +8,8 @@ C=semilayer-wise-mixed-precision-quantization_amd/csrc
 OUT=abl
 mkdir -p $OUT
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off"
-if [ "${STEM:-0}" = 1 ]; then ABL=stem_pool; DEF=SMPQ_SP_DIAG; FIXED="abi quant conv eval fingerprint conv_glds conv_tail"
-else ABL=conv_glds; DEF=SMPQ_DIAG_ABLATE; FIXED="abi quant conv eval fingerprint stem_pool conv_tail"; fi
+if [ "${STEM:-0}" = 1 ]; then ABL=stem_pool; DEF=SMPQ_SP_DIAG; FIXED="abi quant conv eval fingerprint conv_glds"
+else ABL=conv_glds; DEF=SMPQ_DIAG_ABLATE; FIXED="abi quant conv eval fingerprint stem_pool"; fi
 for a in $1; do
   ( /opt/rocm/bin/hipcc $F -D$DEF=$a -c $C/$ABL.hip -o $OUT/g$a.o 2>/dev/null ) &
 done
