@@ -782,6 +782,14 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     if (__any(ovf) && lane == 0) atomicMax(a.overflow, 1);
   }
   SMPQ_STAMP(22);
+#ifdef SMPQ_STAMPS
+  if (lane == 0) {  // slot 23: the CU this wave ran on (XCC id << 16 | HW_ID CU/SH/SE bits)
+    unsigned id, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    smpq_stamps[((size_t)bid * NW + wave) * 32 + 23] = ((unsigned long long)(xcc & 0xf) << 16) | ((id >> 8) & 0xff);
+  }
+#endif
 }
 
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,

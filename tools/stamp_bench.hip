@@ -129,6 +129,36 @@ int run(int argc, char** argv) {
     for (int w = 1; w < NW; ++w) lo = std::min(lo, bar6[w]), hi = std::max(hi, bar6[w]);
     skew.push_back((double)(hi - lo));
   }
+  // residency: per CU (slot 23), the most blocks alive at one instant and the mean over the kernel
+  double conc_sum = 0;
+  int conc_max = 0, ncu = 0;
+  {
+    std::vector<std::vector<std::pair<unsigned long long, int>>> ev(1 << 20);
+    std::vector<int> used;
+    for (int b = 0; b < blocks; ++b) {
+      const unsigned long long* t = &h[(size_t)b * NW * 32];
+      const unsigned cu = (unsigned)t[23] & 0xfffff;
+      if (ev[cu].empty()) used.push_back((int)cu);
+      ev[cu].push_back({t[0], 1});
+      ev[cu].push_back({t[22], -1});
+    }
+    for (int cu : used) {
+      auto& e = ev[cu];
+      std::sort(e.begin(), e.end());
+      int cur = 0;
+      unsigned long long busy = 0, area = 0, prev = e.front().first;
+      for (auto& x : e) {
+        if (cur > 0) busy += x.first - prev, area += (x.first - prev) * cur;
+        cur += x.second;
+        prev = x.first;
+        conc_max = std::max(conc_max, cur);
+      }
+      conc_sum += busy ? (double)area / busy : 0;
+      ++ncu;
+    }
+  }
+  printf("{\"cus_seen\": %d, \"max_blocks_per_cu\": %d, \"mean_blocks_per_cu_while_busy\": %.2f}\n", ncu, conc_max,
+         ncu ? conc_sum / ncu : 0.0);
   printf("{\"shape\": \"%dx%d %d->%d at %d^2, B=%d, BK=%d\", \"blocks\": %d, \"ksteps\": %d, \"kernel_us\": %.1f, "
          "\"median_cycles\": {\"prologue\": %.0f, \"per_k_step\": %.0f, \"step6_barrier_to_frags\": %.0f, "
          "\"step6_dma_issue\": %.0f, \"step6_mfma_issue_to_retire\": %.0f, \"step6_to_next_barrier\": %.0f, "

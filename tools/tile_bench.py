@@ -36,6 +36,7 @@ SHAPES = [  # name, cin, cout, k, stride, hin, residual, wlimbs
     ("ds_1024_2048_14s2", 1024, 2048, 1, 2, 14, False, 3),
     ("ds_512_1024_28s2", 512, 1024, 1, 2, 28, False, 3),
     ("ds_256_512_56s2", 256, 512, 1, 2, 56, False, 3),
+    ("ds_64_256_56", 64, 256, 1, 1, 56, False, 3),
 ]
 dev = torch.device("cuda")
 for name, cin, cout, k, s, h, res, wl in SHAPES:
