@@ -203,27 +203,6 @@ int smpq_conv2d_fwd_q_km(const int8_t* xq, const float* x_absmax, int n, int h, 
                          float* y_absmax, int8_t* yq, float yq_range, int32_t* overflow,
                          const int8_t* residual_q, float residual_range, int tile_cfg, smpq_stream_t stream);
 
-/* A static-range conv (one weight limb) fused with the 1x1 / stride 1 / ReLU conv that follows it
- * in the network — a Bottleneck's conv3 (+ residual) and the next block's conv1 (resnet.py:97-116):
- * every tile holds all cout channels of its pixels, stages its output limb planes in LDS, writes
- * them to yq (the next block's residual) and runs the next conv on them from LDS, writing that
- * conv's limb planes to next_yq [limbs][n][ho][wo][next_cout] with its static range next_yq_range
- * (next_x_absmax: the per-image range of yq as the next conv's input, i.e. yq_range per image).
- * yq and next_yq are bitwise those of smpq_conv2d_fwd_q_km followed by smpq_conv2d_fwd_q_km of the
- * next conv; one overflow flag covers both. limbs 3; next_codes [next_cout][cout], one limb, no
- * offsets; next_cout 64, 128 or 256; tile_cfg -1 = the first fused tile that takes the shape
- * (smpq_conv2d_next_tile_supported). Replaces the pair of nn.Conv2d forwards of
- * resnet.py:104-111 -> 102-104 of the next block. */
-int smpq_conv2d_fwd_q_next(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin, const int8_t* codes,
-                           const int8_t* codes_kmajor, const int32_t* offset, int cout, int kh, int kw, int stride,
-                           int pad, const float* col_scale, const float* col_shift, int relu, int limbs, int8_t* yq,
-                           float yq_range, int32_t* overflow, const int8_t* residual_q, float residual_range,
-                           const int8_t* next_codes, int next_cout, const float* next_x_absmax,
-                           const float* next_col_scale, const float* next_col_shift, int8_t* next_yq,
-                           float next_yq_range, int tile_cfg, smpq_stream_t stream);
-int smpq_conv2d_next_num_tile_configs(void);
-int smpq_conv2d_next_tile_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int next_cout);
-
 /* codes [wlimbs][cout][K] (K % 64 == 0, 16-B aligned) -> out [wlimbs][K/64][cout][64], the K-major
  * copy smpq_conv2d_fwd_q_km reads. */
 int smpq_weights_kmajor(const int8_t* codes, int wlimbs, int cout, int K, int8_t* out, smpq_stream_t stream);

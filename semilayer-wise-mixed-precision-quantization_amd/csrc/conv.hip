@@ -985,52 +985,6 @@ extern "C" int smpq_conv2d_fwd_q_km(const int8_t* xq, const float* x_absmax, int
   return dispatch_limbs<2>(tile_cfg, smallc, limbs, wlimbs, a, s);
 }
 
-extern "C" int smpq_conv2d_fwd_q_next(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
-                                      const int8_t* codes, const int8_t* codes_kmajor, const int32_t* offset, int cout,
-                                      int kh, int kw, int stride, int pad, const float* col_scale,
-                                      const float* col_shift, int relu, int limbs, int8_t* yq, float yq_range,
-                                      int32_t* overflow, const int8_t* residual_q, float residual_range,
-                                      const int8_t* next_codes, int next_cout, const float* next_x_absmax,
-                                      const float* next_col_scale, const float* next_col_shift, int8_t* next_yq,
-                                      float next_yq_range, int tile_cfg, smpq_stream_t stream) {
-  if (!yq || !next_codes || !next_x_absmax || !next_col_scale || !next_col_shift || !next_yq || !(next_yq_range > 0.f))
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd_q_next: null pointer or non-positive range");
-  ConvArgs a;
-  const int rc = conv_args_q(xq, x_absmax, n, h, w, cin, codes, 1, offset, cout, kh, kw, stride, pad, col_scale,
-                             col_shift, nullptr, relu, limbs, nullptr, nullptr, yq, yq_range, overflow, residual_q,
-                             residual_range, a);
-  if (rc) return rc;
-  if (cin % kKStep != 0) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd_q_next: cin must be a multiple of 64");
-  if (tile_cfg < 0) {
-    for (int c = 0; c < next_num_cfgs() && tile_cfg < 0; ++c)
-      if (next_supported(c, cin, cout, kh, kw, limbs, next_cout)) tile_cfg = c;
-    if (tile_cfg < 0) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd_q_next: no fused tile takes this shape");
-  }
-  if (codes_kmajor) {
-    a.codes = codes_kmajor;
-    a.w_kmajor = 1;
-  }
-  a.nx_codes = next_codes;
-  a.nx_cout = next_cout;
-  a.nx_absmax = next_x_absmax;
-  a.nx_col_scale = next_col_scale;
-  a.nx_col_shift = next_col_shift;
-  a.nx_yq = next_yq;
-  a.nx_yq_inv = (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f)) / next_yq_range;
-  static const int nx_ablate = [] {
-    const char* e = getenv("SMPQ_NX_ABLATE");
-    return e ? atoi(e) : 0;
-  }();
-  a.nx_ablate = nx_ablate;
-  return launch_glds_next(tile_cfg, limbs, a, (hipStream_t)stream);
-}
-
-extern "C" int smpq_conv2d_next_num_tile_configs(void) { return next_num_cfgs(); }
-
-extern "C" int smpq_conv2d_next_tile_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int next_cout) {
-  return next_supported(cfg, cin, cout, kh, kw, limbs, next_cout) ? 1 : 0;
-}
-
 extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                                  const int8_t* codes, int wlimbs, const int32_t* offset, int cout, int kh,
                                  int kw, int stride, int pad, const float* col_scale,

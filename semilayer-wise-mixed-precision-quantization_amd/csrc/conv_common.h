@@ -39,19 +39,6 @@ struct ConvArgs {
   // the 64-B K slices of 16 consecutive output channels are one contiguous KiB, so every weight
   // DMA piece is whole cache lines instead of 16 half lines
   int w_kmajor;
-  // Fused next 1x1 conv (smpq_conv2d_fwd_q_next, LDS-DMA tiles that hold ALL cout channels of
-  // their pixels): the block's staged output tile [L][BP][cout] is the activation operand of the
-  // next block's conv1 (1x1, stride 1, cin = cout, one weight limb, no offsets, ReLU), whose
-  // lean static-range epilogue writes its limb planes; the output limb planes are still written
-  // (the next block's residual / downsample input).
-  const int8_t* nx_codes;  // [nx_cout][cout] weight codes of the next conv (row-major)
-  const float* nx_absmax;  // [n] per-image range of this output as the next conv's input
-  const float* nx_col_scale;
-  const float* nx_col_shift;
-  int8_t* nx_yq;    // [L][M][nx_cout] the next conv's output limb planes
-  float nx_yq_inv;  // QMAX / range of the next conv's output quantizer
-  int nx_cout;
-  int nx_ablate;  // diagnostics only (SMPQ_NX_ABLATE): 1 no next-conv stores, 2 no next-conv MFMAs
 };
 
 // Division by a runtime constant d >= 1 for numerators in [0, 2^31): p = 31 + ceil(log2 d),
@@ -97,9 +84,6 @@ void glds_cfg_info(int cfg, int* bm, int* bn, int* threads);
 int glds_cfg_bk(int cfg);
 bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs);
 int launch_glds(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s);
-int next_num_cfgs();
-bool next_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int nx_cout);
-int launch_glds_next(int cfg, int limbs, const ConvArgs& a, hipStream_t s);
 int glds_default_cfg(const ConvArgs& a, int limbs, int wlimbs);
 
 // The 4 codes (channels 0..3) held by one dword per limb plane, w[l] = the 4 balanced digits of

@@ -66,10 +66,8 @@ __device__ unsigned long long* smpq_stamps;
 // scale / shift and the residual scale, ReLU and the code clamp are one v_med3, and overflow is
 // tracked on the rounded codes — about half the VALU work of the general epilogue per output.
 // The body of one block (block `bid` of `total` blocks of this conv); `lds` = the dynamic LDS.
-// NX > 0: the fused next 1x1 conv with NX output channels (ConvArgs nx_*; LEAN epilogue, staged
-// output tile holding all cout channels of the block's pixels).
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
-          bool LEAN = false, bool PIPE = false, int NX = 0>
+          bool LEAN = false, bool PIPE = false>
 __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, int8_t* lds) {
   static_assert(BK == 64 || BK == 128, "BK");
   static_assert(!S2D || BK == 64, "the s2d stem uses 64-B K steps");
@@ -385,17 +383,11 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   // wait until this wave's DMA of step `ready` has landed (younger steps may still fly)
   auto wait_step = [&](int ready) {
     const int d = nissued - ready - 1;  // steps issued after it
-    if constexpr (NST >= 2) {
-      if (kUniform && d == NST - 1) {
-        wait_vm<PPW * (NST - 1)>();
-        return;
-      }
-      if (kUniform && d == NST - 2) {
-        wait_vm<PPW * (NST - 2)>();
-        return;
-      }
-    }
-    {
+    if (kUniform && d == NST - 1) {
+      wait_vm<PPW * (NST - 1)>();
+    } else if (kUniform && d == NST - 2) {
+      wait_vm<PPW * (NST - 2)>();
+    } else {
       wait_vmcnt(d * ppw);
     }
   };
@@ -447,30 +439,6 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  } else if constexpr (NST == 1) {
-    // One LDS stage (round 3): the DMA of step ks + 1 refills the stage once every wave has its
-    // fragments of step ks in registers (a second barrier per step) and flies under step ks's last
-    // MFMAs. Half the LDS of two stages: with 128-B K steps the 128 x 64 tile needs 40 KiB, so a
-    // third block shares the CU (two 80-KiB stages allow two; profiles/r03_residency.txt).
-    issue_next();
-    SMPQ_STAMP(1);
-    for (int ks = 0; ks < nsteps; ++ks) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of step ks has landed
-      __builtin_amdgcn_s_barrier();                     // ... and every wave's
-      asm volatile("" ::: "memory");
-      Frags f;
-#pragma unroll
-      for (int h = 0; h < KH; ++h) {
-        read_frags(f, lds, h);
-        mma(f);
-      }
-      if (ks + 1 < nsteps) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's fragment reads are done
-        __builtin_amdgcn_s_barrier();                       // ... and every wave's: refill the stage
-        asm volatile("" ::: "memory");
-        issue_next();
-      }
-    }
   } else {
 #pragma unroll
     for (int st = 0; st < NST - 1; ++st)
@@ -521,22 +489,6 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   }
 
   SMPQ_STAMP(21);
-  // fused next conv: its weight fragments (A operand, straight from L2 into registers) are requested
-  // now and land under this conv's epilogue. Channel blocks cb = wave + NW * t of the NX outputs,
-  // K = this conv's cout (the staged tile's channels) in 64-B steps.
-  constexpr int NCBW = NX > 0 ? NX / 16 / NW : 1, KS1 = NX > 0 ? BC / 64 : 1;
-  static_assert(NX == 0 || (NX % (16 * NW) == 0 && BC % 64 == 0 && TRT && LEAN && LW == 1),
-                "fused next conv: NX / 16 channel blocks over the waves, whole staged tile, lean epilogue");
-  v4i nxa[NCBW][KS1];
-  if constexpr (NX > 0) {
-    const auto nrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.nx_codes), 0, NX * BC, 0x00020000);
-#pragma unroll
-    for (int t = 0; t < NCBW; ++t)
-#pragma unroll
-      for (int ks = 0; ks < KS1; ++ks)
-        nxa[t][ks] = __builtin_amdgcn_raw_buffer_load_b128(
-            nrs, (unsigned)(((wave + NW * t) * 16 + frow) * BC + 64 * ks + 16 * (lane >> 4)), 0, 0);
-  }
   if constexpr ((kAblate & 16) != 0) {  // diagnostic: no epilogue at all (keep the MFMAs live)
     int keep = 0;
 #pragma unroll
@@ -815,67 +767,6 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
                           __builtin_amdgcn_readfirstlane((unsigned)((long long)l * oplane)), nt);
         }
       }
-      if constexpr (NX > 0) {
-        // The next block's conv1 on the staged tile (activation operand: row rt = pixel, 16-B chunk c
-        // = channels 16c..16c+15 of limb l at chunk c ^ swze<BC>(rt & 15)): exact int32 limb
-        // accumulators, then conv_glds's own lean epilogue (same folded scales, same rounding), so
-        // its limb planes are bitwise those of a separate launch of that conv.
-        constexpr int PB = BP / 16;
-        v4i nacc[L][NCBW][PB];
-#pragma unroll
-        for (int l = 0; l < L; ++l)
-#pragma unroll
-          for (int t = 0; t < NCBW; ++t)
-#pragma unroll
-            for (int pb = 0; pb < PB; ++pb) nacc[l][t][pb] = v4i{0, 0, 0, 0};
-#pragma unroll
-        for (int ks = 0; ks < KS1; ++ks)
-#pragma unroll
-          for (int l = 0; l < L; ++l)
-#pragma unroll
-            for (int pb = 0; pb < PB; ++pb) {
-              const int rt = pb * 16 + frow;
-              const v4i b = *reinterpret_cast<const v4i*>(
-                  lds + l * BP * BC + rt * BC + 16 * ((4 * ks + (lane >> 4)) ^ swze<BC>(frow)));
-              if (a.nx_ablate & 2) {
-                nacc[l][0][pb][0] ^= b[0];
-                continue;
-              }
-#pragma unroll
-              for (int t = 0; t < NCBW; ++t)
-                nacc[l][t][pb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(nxa[t][ks], b, nacc[l][t][pb], 0, 0, 0);
-            }
-        const float ninv = a.nx_yq_inv;
-        const long long nplane = (long long)a.M * NX;
-        const auto nqrs = __builtin_amdgcn_make_buffer_rsrc(a.nx_yq, 0, (int)(L * nplane), 0x00020000);
-        float nmax = 0.f;
-        const int dummy[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int pb = 0; pb < PB; ++pb) {
-          const int m = m0 + pb * 16 + frow;
-          const bool ok = m < a.M;
-          const float rsc = ok ? a.nx_absmax[fast_div(m, a.hw_mul, a.hw_shr)] * a.inv_qmax : 0.f;
-#pragma unroll
-          for (int t = 0; t < NCBW; ++t) {
-            const int c = (wave + NW * t) * 16 + 4 * (lane >> 4);
-            const float4 cs = *reinterpret_cast<const float4*>(a.nx_col_scale + c);
-            const float4 csh = *reinterpret_cast<const float4*>(a.nx_col_shift + c);
-            const float csq[4] = {cs.x * ninv, cs.y * ninv, cs.z * ninv, cs.w * ninv};
-            const float shq[4] = {csh.x * ninv, csh.y * ninv, csh.z * ninv, csh.w * ninv};
-            v4i accq[L];
-#pragma unroll
-            for (int l = 0; l < L; ++l) accq[l] = nacc[l][t][pb];
-            unsigned nw[L];
-            const float mx = lean_quad<L, L, 0>(accq, rsc, csq, shq, false, dummy, 0.f, true, 0.f, nw);
-            nmax = ok ? fmaxf(nmax, mx) : nmax;
-            const unsigned noff = (ok && !(a.nx_ablate & 1)) ? (unsigned)(m * NX + c) : kOOB;
-#pragma unroll
-            for (int l = 0; l < L; ++l)
-              __builtin_amdgcn_raw_buffer_store_b32(nw[l], nqrs, noff, (unsigned)((long long)l * nplane), 0);
-          }
-        }
-        if (__any(nmax > qmax) && lane == 0) atomicMax(a.overflow, 1);
-      }
     } else {
 #pragma unroll
       for (int i = 0; i < WC; ++i)
@@ -902,11 +793,10 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 }
 
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
-          bool LEAN = false, bool PIPE = false, int NX = 0>
+          bool LEAN = false, bool PIPE = false>
 __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // min(NST, ksteps) stages
-  qconv_glds_body<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, LEAN, PIPE, NX>(a, blockIdx.x, gridDim.x,
-                                                                                     lds);
+  qconv_glds_body<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, LEAN, PIPE>(a, blockIdx.x, gridDim.x, lds);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -961,12 +851,6 @@ constexpr GldsCfg kGlds[] = {
     {2, 2, 4, 2, 4, 64, 1},   // 34: as 22
     {1, 4, 4, 1, 4, 64, 1},   // 35: as 24
     {2, 2, 2, 2, 3, 128, 1},  // 36: as 26
-    // one LDS stage of 128-B K steps, 3 waves per SIMD: three blocks per CU (round 3)
-    {2, 2, 2, 2, 1, 128, 0},  // 37: 64 ch x 64 px (waves 32 x 32)
-    {4, 1, 4, 2, 1, 128, 0},  // 38: 256 ch x 32 px
-    {2, 2, 4, 1, 1, 128, 0},  // 39: 128 ch x 32 px
-    {4, 1, 4, 1, 1, 128, 0},  // 40: 256 ch x 16 px, 4 waves per SIMD
-    {1, 4, 4, 1, 1, 128, 0},  // 41: 64 ch x 64 px (waves 64 x 16), 4 waves per SIMD
 };
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
@@ -1105,11 +989,6 @@ static int launch_cfg(int cfg, const ConvArgs& a, hipStream_t s) {
     case 34: return launch_one<L, LW, 2, 2, 4, 2, false, 4, 2, 64, true>(a, s);
     case 35: return launch_one<L, LW, 1, 4, 4, 1, false, 4, 2, 64, true>(a, s);
     case 36: return launch_one<L, LW, 2, 2, 2, 2, false, 3, 2, 128, true>(a, s);
-    case 37: return launch_one<L, LW, 2, 2, 2, 2, false, 1, 3, 128>(a, s);
-    case 38: return launch_one<L, LW, 4, 1, 4, 2, false, 1, 3, 128>(a, s);
-    case 39: return launch_one<L, LW, 2, 2, 4, 1, false, 1, 3, 128>(a, s);
-    case 40: return launch_one<L, LW, 4, 1, 4, 1, false, 1, 4, 128>(a, s);
-    case 41: return launch_one<L, LW, 1, 4, 4, 1, false, 1, 4, 128>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   }
 }
@@ -1123,102 +1002,6 @@ static int launch_s2d(int cfg, const ConvArgs& a, hipStream_t s) {
     case 3: return launch_one<L, LW, 1, 4, 4, 1, true>(a, s);
     case 4: return launch_one<L, LW, 1, 4, 4, 2, true>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: tile config not built for the stem");
-  }
-}
-
-// ---- fused next 1x1 conv (smpq_conv2d_fwd_q_next) ---------------------------------------------
-// Tiles that hold all cout channels of their pixels (BC == cout), 64-B K steps, two stages, the
-// lean static-range epilogue; NX = the next conv's output channels.
-struct NextCfg {
-  int wavesc, wavesp, wc, wp, bc;
-};
-constexpr NextCfg kNext[] = {
-    {4, 1, 4, 2, 256},  // 0: 256 ch x 32 px, 4 waves of 64 x 32
-    {4, 1, 4, 1, 256},  // 1: 256 ch x 16 px
-    {8, 1, 4, 1, 512},  // 2: 512 ch x 16 px, 8 waves of 64 x 16
-    {8, 1, 4, 2, 512},  // 3: 512 ch x 32 px, 8 waves of 64 x 32
-    {4, 1, 8, 1, 512},  // 4: 512 ch x 16 px, 4 waves of 128 x 16
-};
-constexpr int kNumNext = sizeof(kNext) / sizeof(kNext[0]);
-
-int next_num_cfgs() { return kNumNext; }
-
-bool next_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int nx_cout) {
-  if (cfg < 0 || cfg >= kNumNext || limbs != 3 || cin % 64 != 0) return false;
-  const NextCfg& c = kNext[cfg];
-  if (c.bc != cout) return false;
-  const int nw = c.wavesc * c.wavesp;
-  if (!(nx_cout == 64 || nx_cout == 128 || nx_cout == 256) || nx_cout % (16 * nw) != 0) return false;
-  if (nx_cout / 16 / nw * (cout / 64) > 16) return false;  // the next conv's weight fragments: <= 64 VGPRs
-  const int bp = 16 * c.wp * c.wavesp, stage = (cout + limbs * bp) * 64, nsteps = kh * kw * cin / 64;
-  const int tile = limbs * bp * cout;
-  int lds = (nsteps < 2 ? nsteps : 2) * stage;
-  lds = (lds > tile ? lds : tile) + tile;
-  return lds <= 160 * 1024;
-}
-
-template <int L, int WAVES_C, int WAVES_P, int WC, int WP, int NX, int MINW>
-static int launch_one_next(const ConvArgs& a, hipStream_t stream) {
-  constexpr int BC = 16 * WC * WAVES_C, BP = 16 * WP * WAVES_P, BK = 64, NST = 2;
-  const long mt = (a.M + BP - 1) / BP;
-  constexpr int STAGE = (BC + L * BP) * BK;
-  const int nsteps = a.ksteps;
-  constexpr int TILEB = L * BP * BC;
-  int lds_bytes = (nsteps < NST ? nsteps : NST) * STAGE;
-  if (TILEB > lds_bytes) lds_bytes = TILEB;
-  if (a.res_q) lds_bytes += TILEB;
-  constexpr int kMaxLds = 160 * 1024;
-  if (lds_bytes > kMaxLds) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd_q_next: tile needs more LDS than a CU has");
-  constexpr int kMaxNeed = (NST * STAGE > TILEB ? NST * STAGE : TILEB) + TILEB;
-  ConvArgs b = a;
-  fast_div_init(1, b.ntc_mul, b.ntc_shr);
-  auto k = qconv_glds_kernel<L, 1, WAVES_C, WAVES_P, WC, WP, MINW, false, NST, BK, true, false, NX>;
-  static const hipError_t attr = [&] {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             kMaxNeed < kMaxLds ? kMaxNeed : kMaxLds);
-    if (e != hipSuccess) (void)hipGetLastError();
-    return e;
-  }();
-  if (attr != hipSuccess) return check_hip(attr, "qconv_glds_kernel (next) LDS attribute");
-  hipLaunchKernelGGL(k, dim3((unsigned)mt), dim3(64 * WAVES_C * WAVES_P), lds_bytes, stream, b);
-  return check_hip(hipGetLastError(), "qconv_glds_kernel (next) launch");
-}
-
-template <int NX, int NW, int BC>
-constexpr bool next_built() {
-  return NX % (16 * NW) == 0 && NX / 16 / NW * (BC / 64) <= 16;
-}
-
-template <int WAVES_C, int WAVES_P, int WC, int WP, int MINW>
-static int launch_next_nx(const ConvArgs& a, hipStream_t s) {
-  constexpr int NW = WAVES_C * WAVES_P, BC = 16 * WC * WAVES_C;
-  switch (a.nx_cout) {
-    case 64:
-      if constexpr (next_built<64, NW, BC>()) return launch_one_next<3, WAVES_C, WAVES_P, WC, WP, 64, MINW>(a, s);
-      break;
-    case 128:
-      if constexpr (next_built<128, NW, BC>()) return launch_one_next<3, WAVES_C, WAVES_P, WC, WP, 128, MINW>(a, s);
-      break;
-    case 256:
-      if constexpr (next_built<256, NW, BC>()) return launch_one_next<3, WAVES_C, WAVES_P, WC, WP, 256, MINW>(a, s);
-      break;
-    default:
-      break;
-  }
-  return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd_q_next: next conv's output channels not built for this tile");
-}
-
-int launch_glds_next(int cfg, int limbs, const ConvArgs& a, hipStream_t s) {
-  if (limbs != 3 || !next_supported(cfg, a.cin, a.cout, a.kh, a.kw, limbs, a.nx_cout) ||
-      !glds_planes_ok(a, limbs, 1) || (long long)limbs * a.M * a.nx_cout > 0x7fffff00LL)
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd_q_next: tile config does not take this shape");
-  switch (cfg) {
-    case 0: return launch_next_nx<4, 1, 4, 2, 2>(a, s);
-    case 1: return launch_next_nx<4, 1, 4, 1, 2>(a, s);
-    case 2: return launch_next_nx<8, 1, 4, 1, 2>(a, s);
-    case 3: return launch_next_nx<8, 1, 4, 2, 2>(a, s);
-    case 4: return launch_next_nx<4, 1, 8, 1, 2>(a, s);
-    default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd_q_next: bad tile config");
   }
 }
 

@@ -54,11 +54,6 @@ _PROTOS = {
                                _vp, _i, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, ctypes.c_float, _i, _vp]),
     "smpq_conv2d_fwd_q_km": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp,
                                   _vp, _i, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, ctypes.c_float, _i, _vp]),
-    "smpq_conv2d_fwd_q_next": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _i,
-                                    _vp, ctypes.c_float, _vp, _vp, ctypes.c_float, _vp, _i, _vp, _vp, _vp, _vp,
-                                    ctypes.c_float, _i, _vp]),
-    "smpq_conv2d_next_num_tile_configs": (_i, []),
-    "smpq_conv2d_next_tile_supported": (_i, [_i] * 7),
     "smpq_weights_kmajor": (_i, [_vp, _i, _i, _i, _vp, _vp]),
     "smpq_maxpool_limbs": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "smpq_image_quantize_s2d": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp]),

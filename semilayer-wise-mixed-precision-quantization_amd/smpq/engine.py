@@ -67,10 +67,6 @@ FUSED_STEM = [_os.environ.get("SMPQ_FUSED_STEM", "1") != "0"]
 CONCURRENT_DS = [_os.environ.get("SMPQ_CONCURRENT_DS", "1") != "0"]
 # static range: the batch split into this many slices, each on its own stream (concurrent kernels)
 STREAMS = [int(_os.environ.get("SMPQ_STREAMS", "2"))]
-# static range: a Bottleneck's conv3 (+ residual) and the next block's conv1 as ONE launch
-# (ops.tuned_conv2d_q_next: the conv3 output tile stays in LDS as conv1's operand; both outputs
-# bitwise those of the two launches)
-FUSE_NEXT = [_os.environ.get("SMPQ_FUSE_NEXT", "1") != "0"]
 stats.setdefault("graph_captures", 0)
 stats.setdefault("graph_replays", 0)
 
@@ -93,11 +89,10 @@ def get_range_mode():
 
 
 class Act:
-    __slots__ = ("f32", "q", "amax", "rng", "pre")
+    __slots__ = ("f32", "q", "amax", "rng")
 
     def __init__(self, f32=None, q=None, amax=None, rng=None):
         self.f32, self.q, self.amax, self.rng = f32, q, amax, rng  # rng: static range (float) or None
-        self.pre = None  # (conv, Act): that conv's output, computed by the launch that made this Act
 
     def limbs(self):
         if self.q is None:
@@ -230,46 +225,6 @@ def run_conv(conv, bn, act, relu, residual=None, want_amax=True, ctx=None, want_
     return Act(f32=y, amax=yam)
 
 
-def _next_fusable(conv, bn, act, residual, nconv, nbn, ctx):
-    """Plans of (conv, next conv) when the pair can run as one smpq_conv2d_fwd_q_next launch:
-    static ranges, 3 limbs, both convs exact 8-bit codes (one weight limb), the next conv 1x1 /
-    stride 1 on conv's whole output without offsets, a fused tile for the shape. Else None."""
-    if not (FUSE_NEXT[0] and ctx is not None and ctx.ranges is not None and ops.get_act_limbs() == 3
-            and isinstance(conv, QConv2d) and isinstance(nconv, QConv2d) and id(conv) in ctx.ranges
-            and id(nconv) in ctx.ranges and act.q is not None and nconv.kernel_size == (1, 1)
-            and nconv.stride == (1, 1) and nconv.padding == (0, 0) and nconv.groups == 1
-            and nconv.in_channels == conv.out_channels):
-        return None
-    if residual is not None and not (isinstance(residual, Act) and residual.f32 is None and residual.q is not None
-                                     and residual.rng is not None):
-        return None
-    p1, p2 = conv_plan(conv, bn), conv_plan(nconv, nbn)
-    if p1 is None or p2 is None or p1[4] != "exact8" or p2[4] != "exact8" or p2[1] is not None:
-        return None
-    if not ops.next_tile_configs(conv.in_channels, conv.out_channels, conv.kernel_size[0], nconv.out_channels):
-        return None
-    return p1, p2
-
-
-def run_conv_next(conv, bn, act, residual, nconv, plans, ctx):
-    """relu(bn(conv(x)) + residual) and the next conv's relu(bn(nconv(.))) on it, one launch:
-    returns the output Act, carrying the next conv's output Act in ``pre``."""
-    (codes, offset, col_scale, col_shift, _), (ncodes, _, ncs, nsh, _) = plans
-    rng, nrng = ctx.ranges[id(conv)], ctx.ranges[id(nconv)]
-    res_q = res_rng = None
-    if residual is not None:
-        res_q, res_rng = residual.q, residual.rng
-    stats["hip_conv"] += 2
-    conv.last_path = nconv.last_path = "hip-exact8-fused-next"
-    yam = ctx.range_tensor(conv)
-    yq, nq = ops.tuned_conv2d_q_next(act.limbs(), act.amax, codes, offset, conv.kernel_size[0], conv.kernel_size[1],
-                                     conv.stride[0], conv.padding[0], col_scale, col_shift, rng, ctx.overflow,
-                                     ncodes, yam, ncs, nsh, nrng, relu=True, residual_q=res_q, residual_range=res_rng)
-    y = Act(q=yq, amax=yam, rng=rng)
-    y.pre = (nconv, Act(q=nq, amax=ctx.range_tensor(nconv), rng=nrng))
-    return y
-
-
 _STREAMS = {}
 
 
@@ -286,7 +241,7 @@ def _side_stream(device, lane):
     return _stream((device, "ds", lane))
 
 
-def block_forward(blk, x, ctx=None, last=False, nxt=None):
+def block_forward(blk, x, ctx=None, last=False):
     """One BasicBlock / Bottleneck on an Act; returns the output Act. In static mode no
     activation is stored in fp32 except the downsample's identity and the last block's output
     (avgpool): the identity of a block without downsample is read from its input's limb planes.
@@ -324,17 +279,10 @@ def block_forward(blk, x, ctx=None, last=False, nxt=None):
         if side is not None:
             torch.cuda.current_stream().wait_stream(side)
 
-    if x.pre is not None and x.pre[0] is blk.conv1:
-        t1 = x.pre[1]  # computed by the previous block's conv3 launch (run_conv_next)
-    else:
-        t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
+    t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
     if hasattr(blk, "conv3"):  # Bottleneck (resnet.py:97-116)
         t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
         join()
-        plans = None if (last or nxt is None) else \
-            _next_fusable(blk.conv3, blk.bn3, t2, identity, nxt.conv1, nxt.bn1, ctx)
-        if plans is not None:
-            return run_conv_next(blk.conv3, blk.bn3, t2, identity, nxt.conv1, plans, ctx)
         return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax,
                         want_f32=last)
     # BasicBlock (resnet.py:55-68)
@@ -438,8 +386,7 @@ def _features(model, x, ctx):
     act = stem_forward(model, x, ctx)
     blocks = _blocks(model)
     for i, blk in enumerate(blocks):
-        act = block_forward(blk, act, ctx, last=(i == len(blocks) - 1),
-                            nxt=blocks[i + 1] if i + 1 < len(blocks) else None)
+        act = block_forward(blk, act, ctx, last=(i == len(blocks) - 1))
     return act.f32
 
 
@@ -637,7 +584,7 @@ def _static_eager(model, x, cal):
 
 def _graph_key(model, x, cal):
     return (tuple(x.shape), x.dtype, x.device, cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0],
-            CONCURRENT_DS[0], STREAMS[0], ops.KMAJOR[0], FUSE_NEXT[0])
+            CONCURRENT_DS[0], STREAMS[0], ops.KMAJOR[0])
 
 
 def _graph_ready(model, x, cal):

@@ -480,106 +480,6 @@ def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_sh
     return out
 
 
-def conv2d_q_next(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift, emit_range, overflow,
-                  next_codes, next_x_absmax, next_col_scale, next_col_shift, next_range, relu=True,
-                  residual_q=None, residual_range=None, tile_cfg=-1):
-    """A static-range conv (lean epilogue: limb planes out) fused with the 1x1 / stride 1 / ReLU conv
-    that consumes its output (a Bottleneck's conv3 + the next block's conv1, resnet.py:97-116):
-    returns (yq, next_yq), bitwise those of conv2d_q(...) followed by conv2d_q on yq. The next conv
-    has one weight limb and no offsets (next_codes [next_cout, cout]); next_x_absmax is yq's
-    per-image range tensor as that conv's input."""
-    _req(xq.is_cuda and xq.dtype == torch.int8 and xq.dim() == 5 and xq.is_contiguous(), "conv: xq must be [L,n,h,w,c] int8")
-    limbs, n, h, w, cin = xq.shape
-    km = getattr(codes, "_smpq_km", None)
-    if codes.dim() == 3:
-        _req(codes.shape[0] == 1, "conv_next: one weight limb")
-        codes = codes[0]
-    cout, K = codes.shape
-    _req(limbs == 3 and codes.dtype == torch.int8 and K == kh * kw * cin and codes.is_contiguous(), "conv_next: codes")
-    if next_codes.dim() == 3:
-        _req(next_codes.shape[0] == 1, "conv_next: next conv has one weight limb")
-        next_codes = next_codes[0]
-    ncout = next_codes.shape[0]
-    _req(next_codes.shape == (ncout, cout) and next_codes.dtype == torch.int8 and next_codes.is_contiguous(),
-         "conv_next: next codes [next_cout, cout]")
-    for t, c in ((col_scale, cout), (col_shift, cout), (next_col_scale, ncout), (next_col_shift, ncout)):
-        _req(t.dtype == torch.float32 and t.numel() == c and t.is_contiguous() and t.device == xq.device,
-             "conv_next: col vectors")
-    _req(offset is None or (offset.dtype == torch.int32 and offset.numel() == cout), "conv_next: offset")
-    _req(next_x_absmax.dtype == torch.float32 and next_x_absmax.numel() == n, "conv_next: next_x_absmax")
-    ho = (h + 2 * pad - kh) // stride + 1
-    wo = (w + 2 * pad - kw) // stride + 1
-    if residual_q is not None:
-        _req(residual_q.shape == (limbs, n, ho, wo, cout) and residual_q.dtype == torch.int8
-             and residual_q.is_contiguous() and residual_range is not None and residual_range > 0, "conv_next: residual_q")
-    yq = torch.empty(limbs, n, ho, wo, cout, dtype=torch.int8, device=xq.device)
-    nyq = torch.empty(limbs, n, ho, wo, ncout, dtype=torch.int8, device=xq.device)
-    lib = _lib.load()
-    hook = _CONV_HOOK[0]
-    if hook is not None:
-        hook.begin()
-    with torch.cuda.device(xq.device):
-        _lib.check(lib.smpq_conv2d_fwd_q_next(
-            _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, cin, _lib.ptr(codes), _lib.ptr(km), _lib.ptr(offset), cout,
-            kh, kw, stride, pad, _lib.ptr(col_scale), _lib.ptr(col_shift), 1 if relu else 0, int(limbs), _lib.ptr(yq),
-            float(emit_range), _lib.ptr(overflow), _lib.ptr(residual_q), float(residual_range or 0.0),
-            _lib.ptr(next_codes), int(ncout), _lib.ptr(next_x_absmax), _lib.ptr(next_col_scale),
-            _lib.ptr(next_col_shift), _lib.ptr(nyq), float(next_range), int(tile_cfg), _lib.stream_ptr()),
-            "smpq_conv2d_fwd_q_next")
-    if hook is not None:
-        # one launch doing two convs: the algorithmic work of both (the intermediate yq is written
-        # once and read from LDS, so its re-read is not counted)
-        a1 = alg_work(n, h, w, cin, cout, kh, kw, ho, wo, limbs, 1, False, True, False, residual_q is not None)
-        a2 = alg_work(n, ho, wo, cout, ncout, 1, 1, ho, wo, limbs, 1, False, True, False, False)
-        ops_ = a1["ops"] + a2["ops"]
-        hook.end({"ops": ops_, "bytes": a1["bytes"] + a2["bytes"] - limbs * n * ho * wo * cout,
-                  "passes": (a1["ops"] * a1["passes"] + a2["ops"] * a2["passes"]) / ops_,
-                  "shape": "%4d->%4d->%4d k%d %3d %s" % (cin, cout, ncout, kh, ho, "r" if residual_q is not None else "-")})
-    return yq, nyq
-
-
-def next_tile_configs(cin, cout, kh, next_cout, limbs=3):
-    """Fused-tile configs (smpq_conv2d_fwd_q_next) that take this shape."""
-    lib = _lib.load()
-    return [c for c in range(lib.smpq_conv2d_next_num_tile_configs())
-            if lib.smpq_conv2d_next_tile_supported(c, int(cin), int(cout), int(kh), int(kh), int(limbs), int(next_cout))]
-
-
-_TUNED_NEXT = {}
-
-
-def tuned_conv2d_q_next(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift, emit_range, overflow,
-                        next_codes, next_x_absmax, next_col_scale, next_col_shift, next_range, relu=True,
-                        residual_q=None, residual_range=None):
-    """conv2d_q_next with the fastest fused tile for this shape (timed once per shape)."""
-    limbs, n, h, w, cin = xq.shape
-    cout = codes.shape[-2]
-    ncout = next_codes.shape[-2]
-    key = (n, h, w, cin, cout, kh, kw, stride, pad, ncout, residual_q is not None)
-    cfg = _TUNED_NEXT.get(key)
-    args = (xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift, emit_range, overflow,
-            next_codes, next_x_absmax, next_col_scale, next_col_shift, next_range)
-    kw_ = dict(relu=relu, residual_q=residual_q, residual_range=residual_range)
-    if cfg is None and AUTOTUNE[0] and not torch.cuda.is_current_stream_capturing():
-        best = None
-        for c in next_tile_configs(cin, cout, kh, ncout, limbs):
-            times = []
-            for rep in range(3):
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record()
-                conv2d_q_next(*args, tile_cfg=c, **kw_)
-                e1.record()
-                times.append((e0, e1))
-            torch.cuda.synchronize()
-            t = min(a.elapsed_time(b) for a, b in times[1:])
-            if best is None or t < best[0]:
-                best = (t, c)
-        cfg = best[1] if best is not None else -1
-        _TUNED_NEXT[key] = cfg
-    return conv2d_q_next(*args, tile_cfg=-1 if cfg is None else cfg, **kw_)
-
-
 # ---- per-shape autotuning of the block tile (cf. cudnn.benchmark=True, resnet50_main.py:10) ----
 AUTOTUNE = [os.environ.get("SMPQ_AUTOTUNE", "1") != "0"]
 # diagnostics (A/B of tile families on one box): tile configs the autotuner never tries
