@@ -66,21 +66,14 @@ __device__ unsigned long long* smpq_stamps;
 // scale / shift and the residual scale, ReLU and the code clamp are one v_med3, and overflow is
 // tracked on the rounded codes — about half the VALU work of the general epilogue per output.
 // The body of one block (block `bid` of `total` blocks of this conv); `lds` = the dynamic LDS.
-// M32: v_mfma_i32_32x32x32_i8 (32 x 32 fragment blocks: half the MFMA instructions of the 16 x 16
-// form for the same work, so twice the issue slots beside each; per-quad epilogue with dword
-// limb-plane loads and stores, no staged tiles). WC / WP then count 32-row blocks.
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
-          bool LEAN = false, bool PIPE = false, bool M32 = false>
+          bool LEAN = false, bool PIPE = false>
 __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, int8_t* lds) {
   static_assert(BK == 64 || BK == 128, "BK");
   static_assert(!S2D || BK == 64, "the s2d stem uses 64-B K steps");
-  static_assert(!M32 || !S2D, "32 x 32 blocks: not for the s2d stem");
-  constexpr int FB = M32 ? 32 : 16;      // rows of one MFMA fragment block
-  constexpr int KQ = M32 ? 2 : 1;        // MFMA K steps per 64-B K slice
-  constexpr int WCE = M32 ? 4 * WC : WC;  // 4-channel accumulator quads per lane and pixel block
   constexpr int NW = WAVES_C * WAVES_P;
-  constexpr int BC = FB * WC * WAVES_C;  // channels per block tile
-  constexpr int BP = FB * WP * WAVES_P;  // pixels per block tile
+  constexpr int BC = 16 * WC * WAVES_C;  // channels per block tile
+  constexpr int BP = 16 * WP * WAVES_P;  // pixels per block tile
   constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
   constexpr int NACC = L + LW - 1 - SMIN;
   constexpr int KH = BK / 64;      // MFMA K steps per stage
@@ -95,7 +88,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   // Epilogue limb-plane tiles in LDS (configs with 4k channel blocks per wave): the residual's
   // tile arrives by DMA at kernel start (whole lines, overlapped with the K loop); the output's is
   // staged in the operand area and copied out row-major (whole lines when BC >= 128 or BC == cout)
-  constexpr bool TRT = !M32 && (WC % 4) == 0;
+  constexpr bool TRT = (WC % 4) == 0;
   constexpr int TILEB = L * BP * BC;
   if constexpr ((kAblate & 32) != 0) {  // diagnostic: static-range epilogue only
     a.y = nullptr;
@@ -201,15 +194,13 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     }
   };
 
-  typedef int v16i __attribute__((ext_vector_type(16)));
-  typedef typename std::conditional<M32, v16i, v4i>::type vacc;
-  vacc acc[NACC][WC][WP];
+  v4i acc[NACC][WC][WP];
 #pragma unroll
   for (int s = 0; s < NACC; ++s)
 #pragma unroll
     for (int i = 0; i < WC; ++i)
 #pragma unroll
-      for (int j = 0; j < WP; ++j) acc[s][i][j] = vacc{};
+      for (int j = 0; j < WP; ++j) acc[s][i][j] = v4i{0, 0, 0, 0};
   const bool do_off = (LW == 1) && a.has_offset;
   int rs[L][WP];  // per-lane partial pixel sums of activation codes (LW == 1 offset correction)
 #pragma unroll
@@ -219,15 +210,9 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 
   // fragment read offset inside a 16-row block of a [rows][BK] region, per MFMA K step h
   const int frow = lane & 15;
-  // (M32: row lane & 31, K half kq: 16-B chunk 2 kq + (lane >> 5) of the 64-B slice; the swizzle
-  // depends on the row within its 16-row group, so the 16-row image serves both forms)
-  int rd[KH][KQ];
+  int rd[KH];
 #pragma unroll
-  for (int h = 0; h < KH; ++h)
-#pragma unroll
-    for (int kq = 0; kq < KQ; ++kq)
-      rd[h][kq] = M32 ? (lane & 31) * BK + 16 * ((4 * h + 2 * kq + (lane >> 5)) ^ swz<BK>(frow))
-                      : frow * BK + 16 * ((4 * h + (lane >> 4)) ^ swz<BK>(frow));
+  for (int h = 0; h < KH; ++h) rd[h] = frow * BK + 16 * ((4 * h + (lane >> 4)) ^ swz<BK>(frow));
   const int nsteps = a.ksteps / KH;  // a.ksteps counts 64-wide K steps
 
   // Output coordinates of this lane: channels chan[i] + 0..3 of pixel mrow[j]; ooff = element
@@ -236,19 +221,16 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   bool mok[WP];
 #pragma unroll
   for (int j = 0; j < WP; ++j) {
-    const int m = m0 + (wp * WP + j) * FB + (M32 ? (lane & 31) : frow);
+    const int m = m0 + (wp * WP + j) * 16 + frow;
     mok[j] = m < a.M;
     mrow[j] = mok[j] ? m : 0;
   }
-  // quad i: M32 block i / 4, rows 8 (i % 4) + 4 (lane >> 5) + 0..3 (the 32 x 32 accumulator layout)
-  int chan[WCE];
+  int chan[WC];
 #pragma unroll
-  for (int i = 0; i < WCE; ++i)
-    chan[i] = M32 ? n0 + (wc * WC + i / 4) * 32 + 8 * (i % 4) + 4 * (lane >> 5)
-                  : n0 + (wc * WC + i) * 16 + 4 * (lane >> 4);
-  unsigned ooff[WCE][WP];
+  for (int i = 0; i < WC; ++i) chan[i] = n0 + (wc * WC + i) * 16 + 4 * (lane >> 4);
+  unsigned ooff[WC][WP];
 #pragma unroll
-  for (int i = 0; i < WCE; ++i)
+  for (int i = 0; i < WC; ++i)
 #pragma unroll
     for (int j = 0; j < WP; ++j)  // cout % 16 == 0: the 4 channels are valid together
       ooff[i][j] = (mok[j] && chan[i] < a.cout) ? (unsigned)(mrow[j] * a.cout + chan[i]) : kOOB;
@@ -272,7 +254,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     }
 
   // residual limb planes: issued now, consumed in the epilogue (latency hidden behind the K loop)
-  int rq[WCE][WP][L];
+  int rq[WC][WP][L];
   const int nst_eff = nsteps < NST ? nsteps : NST;
   const int resoff = (stage_out && TILEB > nst_eff * STAGE) ? TILEB : nst_eff * STAGE;  // LDS layout
   if constexpr (TR) {
@@ -313,7 +295,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.res_q), 0, (int)(L * oplane),
                                                        0x00020000);
 #pragma unroll
-    for (int i = 0; i < WCE; ++i)
+    for (int i = 0; i < WC; ++i)
 #pragma unroll
       for (int j = 0; j < WP; ++j)
 #pragma unroll
@@ -349,23 +331,19 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   int nissued = 0, wbuf = 0, rbuf = 0;
   // fragments of one MFMA K step of a stage
   struct Frags {
-    v4i w[LW][WC][KQ], a[L][WP][KQ];
+    v4i w[LW][WC], a[L][WP];
   };
   auto read_frags = [&](Frags& f, const int8_t* sb, int h) {
 #pragma unroll
-    for (int kq = 0; kq < KQ; ++kq) {
+    for (int lw = 0; lw < LW; ++lw)
 #pragma unroll
-      for (int lw = 0; lw < LW; ++lw)
+      for (int i = 0; i < WC; ++i)
+        f.w[lw][i] = *reinterpret_cast<const v4i*>(sb + (lw * BC + (wc * WC + i) * 16) * BK + rd[h]);
 #pragma unroll
-        for (int i = 0; i < WC; ++i)
-          f.w[lw][i][kq] = *reinterpret_cast<const v4i*>(sb + (lw * BC + (wc * WC + i) * FB) * BK + rd[h][kq]);
+    for (int l = 0; l < L; ++l)
 #pragma unroll
-      for (int l = 0; l < L; ++l)
-#pragma unroll
-        for (int j = 0; j < WP; ++j)
-          f.a[l][j][kq] =
-              *reinterpret_cast<const v4i*>(sb + WPIECES * 1024 + (l * BP + (wp * WP + j) * FB) * BK + rd[h][kq]);
-    }
+      for (int j = 0; j < WP; ++j)
+        f.a[l][j] = *reinterpret_cast<const v4i*>(sb + WPIECES * 1024 + (l * BP + (wp * WP + j) * 16) * BK + rd[h]);
   };
   auto mma = [&](const Frags& f) {
     if (do_off) {
@@ -374,13 +352,10 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 #pragma unroll
         for (int j = 0; j < WP; ++j) {
           int s = rs[l][j];
-#pragma unroll
-          for (int kq = 0; kq < KQ; ++kq) {
-            s = __builtin_amdgcn_sdot4(f.a[l][j][kq].x, 0x01010101, s, false);
-            s = __builtin_amdgcn_sdot4(f.a[l][j][kq].y, 0x01010101, s, false);
-            s = __builtin_amdgcn_sdot4(f.a[l][j][kq].z, 0x01010101, s, false);
-            s = __builtin_amdgcn_sdot4(f.a[l][j][kq].w, 0x01010101, s, false);
-          }
+          s = __builtin_amdgcn_sdot4(f.a[l][j].x, 0x01010101, s, false);
+          s = __builtin_amdgcn_sdot4(f.a[l][j].y, 0x01010101, s, false);
+          s = __builtin_amdgcn_sdot4(f.a[l][j].z, 0x01010101, s, false);
+          s = __builtin_amdgcn_sdot4(f.a[l][j].w, 0x01010101, s, false);
           rs[l][j] = s;
         }
     }
@@ -390,18 +365,11 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       for (int lw = 0; lw < LW; ++lw) {
         if (l + lw < SMIN || (kAblate & 8)) continue;  // compile-time: skipped low-digit product
 #pragma unroll
-        for (int kq = 0; kq < KQ; ++kq)
+        for (int i = 0; i < WC; ++i)
 #pragma unroll
-          for (int i = 0; i < WC; ++i)
-#pragma unroll
-            for (int j = 0; j < WP; ++j) {
-              if constexpr (M32)
-                acc[l + lw - SMIN][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
-                    f.w[lw][i][kq], f.a[l][j][kq], acc[l + lw - SMIN][i][j], 0, 0, 0);
-              else
-                acc[l + lw - SMIN][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
-                    f.w[lw][i][kq], f.a[l][j][kq], acc[l + lw - SMIN][i][j], 0, 0, 0);
-            }
+          for (int j = 0; j < WP; ++j)
+            acc[l + lw - SMIN][i][j] =
+                __builtin_amdgcn_mfma_i32_16x16x64_i8(f.w[lw][i], f.a[l][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
       }
   };
   auto issue_next = [&]() {
@@ -528,26 +496,10 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 #pragma unroll
       for (int i = 0; i < WC; ++i)
 #pragma unroll
-        for (int j = 0; j < WP; ++j) keep ^= acc[q][i][j][0] ^ acc[q][i][j][3];
+        for (int j = 0; j < WP; ++j) keep ^= acc[q][i][j].x ^ acc[q][i][j].w;
     if (keep == 0x7654321) a.overflow[0] = keep;
     return;
   }
-  // the accumulators as 4-channel quads of one pixel (M32: quad i = rows 8 (i % 4) + 4 (lane >> 5)
-  // + 0..3 of 32 x 32 block i / 4 — registers 4 (i % 4) .. + 3)
-  v4i acce[NACC][WCE][WP];
-#pragma unroll
-  for (int s = 0; s < NACC; ++s)
-#pragma unroll
-    for (int i = 0; i < WCE; ++i)
-#pragma unroll
-      for (int j = 0; j < WP; ++j) {
-        if constexpr (M32) {
-          const auto& v = acc[s][i / 4][j];
-          acce[s][i][j] = v4i{v[4 * (i % 4)], v[4 * (i % 4) + 1], v[4 * (i % 4) + 2], v[4 * (i % 4) + 3]};
-        } else {
-          acce[s][i][j] = acc[s][i][j];
-        }
-      }
   // ---- epilogue: straight from the accumulators, in phases (uniform branches per phase) -----
   // accumulator-layout dword (channels 4g..4g+3 of block wc * WC + i, pixel row of block j) of a
   // [L][BP][BC] limb-plane tile in LDS: conflict-free for ds_read_b32 / ds_write_b32 (64 banks)
@@ -579,7 +531,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 #pragma unroll
       for (int j = 0; j < WP; ++j) {
         int s = rs[l][j];
-        if constexpr (!M32) s += __shfl_xor(s, 16, kWave);
+        s += __shfl_xor(s, 16, kWave);
         s += __shfl_xor(s, 32, kWave);
         rs[l][j] = s;
       }
@@ -587,7 +539,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   if constexpr (SMIN == 0) {
     if (do_off) {  // weight offsets (8-bit channels off-centre): acc_l += offset_c * sum of pixel digits_l
 #pragma unroll
-      for (int i = 0; i < WCE; ++i) {
+      for (int i = 0; i < WC; ++i) {
         const int c = chan[i] < a.cout ? chan[i] : 0;
         const int4 coff = *reinterpret_cast<const int4*>(a.w_off + c);
         const int cor[4] = {coff.x, coff.y, coff.z, coff.w};
@@ -597,7 +549,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
           for (int j = 0; j < WP; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r)  // |offset| < 2^15, |pixel sum| < 2^22: full-rate 24-bit multiply
-              acce[s][i][j][r] += __mul24(cor[r], rs[s][j]);
+              acc[s][i][j][r] += __mul24(cor[r], rs[s][j]);
       }
     }
   }
@@ -605,11 +557,11 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 #pragma unroll
   for (int j = 0; j < WP; ++j) rscale[j] = mok[j] ? a.x_absmax[fast_div(mrow[j], a.hw_mul, a.hw_shr)] * a.inv_qmax : 0.f;
   // residual limb planes -> codes, all at once (one LDS wait instead of one per block)
-  int rqv[WCE][WP][4];
+  int rqv[WC][WP][4];
   if (a.res_q) {
-    unsigned rw[WCE][WP][L];
+    unsigned rw[WC][WP][L];
 #pragma unroll
-    for (int i = 0; i < WCE; ++i)
+    for (int i = 0; i < WC; ++i)
 #pragma unroll
       for (int j = 0; j < WP; ++j)
 #pragma unroll
@@ -617,7 +569,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
           rw[i][j][l] = (TR && stage_res) ? *reinterpret_cast<const unsigned*>(lds + tile_word(resoff, i, j, l))
                                           : (unsigned)rq[i][j][l];
 #pragma unroll
-    for (int i = 0; i < WCE; ++i)
+    for (int i = 0; i < WC; ++i)
 #pragma unroll
       for (int j = 0; j < WP; ++j) decode4<L>(rw[i][j], rqv[i][j]);
   }
@@ -628,7 +580,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     f2 v;
 #pragma unroll
     for (int s = 0; s < NACC; ++s) {
-      const int t0 = acce[s][i][j][2 * h], t1 = acce[s][i][j][2 * h + 1];
+      const int t0 = acc[s][i][j][2 * h], t1 = acc[s][i][j][2 * h + 1];
       const f2 tf = f2{(float)t0, (float)t1};
       constexpr float w0 = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
       const float lw = w0 * (float)(1 << (8 * s));
@@ -637,7 +589,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     }
     return v;
   };
-  unsigned wq[WCE][WP][L];
+  unsigned wq[WC][WP][L];
   float vmax = 0.f;
   if constexpr (LEAN) {
     // z = v * (rscale * col_scale / step_out) + col_shift / step_out [+ r * res_scale / step_out];
@@ -649,7 +601,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     const bool has_res = a.res_q != nullptr;
     const bool relu = a.relu != 0;
 #pragma unroll
-    for (int i = 0; i < WCE; ++i) {
+    for (int i = 0; i < WC; ++i) {
       const int c = chan[i] < a.cout ? chan[i] : 0;
       const float4 cs = *reinterpret_cast<const float4*>(a.col_scale + c);
       const float4 csh = *reinterpret_cast<const float4*>(a.col_shift + c);
@@ -659,16 +611,16 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       for (int j = 0; j < WP; ++j) {
         v4i accq[NACC];
 #pragma unroll
-        for (int t = 0; t < NACC; ++t) accq[t] = acce[t][i][j];
+        for (int t = 0; t < NACC; ++t) accq[t] = acc[t][i][j];
         const float m = lean_quad<L, NACC, SMIN>(accq, rscale[j], csq, shq, has_res, rqv[i][j], rsq, relu, lo,
                                                  wq[i][j]);
         vmax = ooff[i][j] != kOOB ? fmaxf(vmax, m) : vmax;
       }
     }
   } else {
-    float o[WCE][WP][4];
+    float o[WC][WP][4];
 #pragma unroll
-    for (int i = 0; i < WCE; ++i) {
+    for (int i = 0; i < WC; ++i) {
       const int c = chan[i] < a.cout ? chan[i] : 0;
       const float4 cs = *reinterpret_cast<const float4*>(a.col_scale + c);
       const float4 csh = *reinterpret_cast<const float4*>(a.col_shift + c);
@@ -690,13 +642,13 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     if (a.residual && !a.res_q) {
       const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.residual), 0, (int)(4 * oplane),
                                                          0x00020000);
-      v4u rv[WCE][WP];
+      v4u rv[WC][WP];
 #pragma unroll
-      for (int i = 0; i < WCE; ++i)
+      for (int i = 0; i < WC; ++i)
 #pragma unroll
         for (int j = 0; j < WP; ++j) rv[i][j] = __builtin_amdgcn_raw_buffer_load_b128(rrs, f32_off(ooff[i][j]), 0, 0);
 #pragma unroll
-      for (int i = 0; i < WCE; ++i)
+      for (int i = 0; i < WC; ++i)
 #pragma unroll
         for (int j = 0; j < WP; ++j)
 #pragma unroll
@@ -704,7 +656,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     }
     if (a.relu) {
 #pragma unroll
-      for (int i = 0; i < WCE; ++i)
+      for (int i = 0; i < WC; ++i)
 #pragma unroll
         for (int j = 0; j < WP; ++j)
 #pragma unroll
@@ -713,7 +665,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     if (a.y) {
       const v4i yrs4 = make_rsrc(a.y, 4LL * oplane);
 #pragma unroll
-      for (int i = 0; i < WCE; ++i)
+      for (int i = 0; i < WC; ++i)
 #pragma unroll
         for (int j = 0; j < WP; ++j) {
           const v4u v = {__float_as_uint(o[i][j][0]), __float_as_uint(o[i][j][1]), __float_as_uint(o[i][j][2]),
@@ -724,7 +676,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     if (a.yq) {
       // fused quantizer of the next conv's input (static range)
 #pragma unroll
-      for (int i = 0; i < WCE; ++i)
+      for (int i = 0; i < WC; ++i)
 #pragma unroll
         for (int j = 0; j < WP; ++j) {
           int q[4];
@@ -747,15 +699,15 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       for (int j = 0; j < WP; ++j) {
         float am = 0.f;
 #pragma unroll
-        for (int i = 0; i < WCE; ++i)
+        for (int i = 0; i < WC; ++i)
           if (ooff[i][j] != kOOB)
 #pragma unroll
             for (int r = 0; r < 4; ++r) am = fmaxf(am, fabsf(o[i][j][r]));
-        if constexpr (!M32) am = fmaxf(am, __shfl_xor(am, 16, kWave));
+        am = fmaxf(am, __shfl_xor(am, 16, kWave));
         pmax[j] = fmaxf(am, __shfl_xor(am, 32, kWave));
       }
-      const int mfirst = m0 + wp * WP * FB;
-      const int mlast = min(mfirst + WP * FB, a.M) - 1;
+      const int mfirst = m0 + wp * WP * 16;
+      const int mlast = min(mfirst + WP * 16, a.M) - 1;
       if (mfirst <= mlast) {
         const int img_lo = fast_div(mfirst, a.hw_mul, a.hw_shr), img_hi = fast_div(mlast, a.hw_mul, a.hw_shr);
         if (img_lo == img_hi) {
@@ -764,7 +716,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
           for (int j = 0; j < WP; ++j) v = fmaxf(v, pmax[j]);
           v = wave_max(v);
           if (lane == 0 && v > 0.f) atomic_max_nonneg(&a.y_absmax[img_lo], v);
-        } else if (lane < FB) {
+        } else if (lane < 16) {
 #pragma unroll
           for (int j = 0; j < WP; ++j)
             if (mok[j] && pmax[j] > 0.f) atomic_max_nonneg(&a.y_absmax[fast_div(mrow[j], a.hw_mul, a.hw_shr)], pmax[j]);
@@ -794,7 +746,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       // read after this barrier), then copy it out row-major in 16-B pieces
       __syncthreads();
 #pragma unroll
-      for (int i = 0; i < WCE; ++i)
+      for (int i = 0; i < WC; ++i)
 #pragma unroll
         for (int j = 0; j < WP; ++j)
 #pragma unroll
@@ -817,7 +769,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < WCE; ++i)
+      for (int i = 0; i < WC; ++i)
 #pragma unroll
         for (int j = 0; j < WP; ++j)
 #pragma unroll
@@ -841,17 +793,16 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 }
 
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
-          bool LEAN = false, bool PIPE = false, bool M32 = false>
+          bool LEAN = false, bool PIPE = false>
 __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // min(NST, ksteps) stages
-  qconv_glds_body<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, LEAN, PIPE, M32>(a, blockIdx.x, gridDim.x,
-                                                                                      lds);
+  qconv_glds_body<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, LEAN, PIPE>(a, blockIdx.x, gridDim.x, lds);
 }
 
 // ------------------------------------------------------------------------------------------
 #ifndef SMPQ_KERNEL_ONLY  // (tools/isa.sh compiles single kernel instances for inspection)
 struct GldsCfg {
-  int wavesc, wavesp, wc, wp, stages, bk, pipe, m32 = 0;  // m32: wc / wp count 32 x 32 blocks
+  int wavesc, wavesp, wc, wp, stages, bk, pipe;
 };
 constexpr GldsCfg kGlds[] = {
     {2, 2, 2, 2, 2, 64, 0},  // 0:  64 ch x  64 px, 256 threads
@@ -900,15 +851,6 @@ constexpr GldsCfg kGlds[] = {
     {2, 2, 4, 2, 4, 64, 1},   // 34: as 22
     {1, 4, 4, 1, 4, 64, 1},   // 35: as 24
     {2, 2, 2, 2, 3, 128, 1},  // 36: as 26
-    // v_mfma_i32_32x32x32_i8 (round 3): the same wave tiles in half the MFMA instructions
-    {2, 2, 2, 1, 2, 64, 0, 1},   // 37: 128 ch x 64 px (waves 64 x 32), as 2
-    {2, 2, 2, 1, 3, 64, 0, 1},   // 38: as 12
-    {2, 2, 2, 1, 2, 128, 0, 1},  // 39: as 18
-    {2, 2, 2, 1, 2, 64, 1, 1},   // 40: as 27 (register-pipelined)
-    {2, 2, 2, 1, 3, 64, 1, 1},   // 41: as 31
-    {4, 1, 2, 1, 2, 64, 0, 1},   // 42: 256 ch x 32 px, as 7
-    {1, 4, 2, 1, 2, 64, 0, 1},   // 43:  64 ch x 128 px (waves 64 x 32)
-    {2, 2, 1, 2, 2, 64, 0, 1},   // 44:  64 ch x 128 px (waves 32 x 64)
 };
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
@@ -922,14 +864,13 @@ bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int w
   if (cin % 64 != 0 || cout % 16 != 0 || (c.bk == 128 && cin % 128 != 0)) return false;
   if (wlimbs == 3 && limbs != 3) return false;
   const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
-  const int fb = c.m32 ? 32 : 16;
-  const int accs = (limbs + wlimbs - 1 - smin) * c.wc * c.wp * (c.m32 ? 16 : 4);
+  const int accs = (limbs + wlimbs - 1 - smin) * c.wc * c.wp * 4;
   if (accs > 128 || (accs == 128 && limbs > 1)) return false;  // (128 at 2 activation limbs spills)
-  const int bc = fb * c.wc * c.wavesc, bp = fb * c.wp * c.wavesp;
+  const int bc = 16 * c.wc * c.wavesc, bp = 16 * c.wp * c.wavesp;
   const int stage = (wlimbs * bc + limbs * bp) * c.bk;
   const int nsteps = kh * kw * cin / c.bk;
   int lds = (nsteps < c.stages ? nsteps : c.stages) * stage;
-  if (!c.m32 && c.wc % 4 == 0) {  // worst case: staged output tile + residual tile (static-range epilogue)
+  if (c.wc % 4 == 0) {  // worst case: staged output tile + residual tile (static-range epilogue)
     const int tile = limbs * bp * bc;
     lds = (lds > tile ? lds : tile) + tile;
   }
@@ -956,20 +897,19 @@ int glds_default_cfg(const ConvArgs& a, int limbs, int wlimbs) {
 
 void glds_cfg_info(int cfg, int* bm, int* bn, int* threads) {
   const GldsCfg& c = kGlds[cfg];
-  *bm = (c.m32 ? 32 : 16) * c.wp * c.wavesp;  // pixels (GEMM rows)
-  *bn = (c.m32 ? 32 : 16) * c.wc * c.wavesc;  // channels
+  *bm = 16 * c.wp * c.wavesp;  // pixels (GEMM rows)
+  *bn = 16 * c.wc * c.wavesc;  // channels
   *threads = 64 * c.wavesc * c.wavesp;
 }
 
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, bool S2D = false, int NST = 2, int MINW = 2,
-          int BK = 64, bool PIPE = false, bool M32 = false>
+          int BK = 64, bool PIPE = false>
 static int launch_one(const ConvArgs& a, hipStream_t stream) {
   constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
-  constexpr int FB = M32 ? 32 : 16;
-  if constexpr ((L + LW - 1 - SMIN) * WC * WP * (M32 ? 16 : 4) > 128) {
+  if constexpr ((L + LW - 1 - SMIN) * WC * WP * 4 > 128) {
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: tile config too large for these limb counts");
   } else {
-    constexpr int BC = FB * WC * WAVES_C, BP = FB * WP * WAVES_P;
+    constexpr int BC = 16 * WC * WAVES_C, BP = 16 * WP * WAVES_P;
     const long mt = (a.M + BP - 1) / BP;
     const long nt = (a.cout + BC - 1) / BC;
     if (mt * nt > 0x7fffffffL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
@@ -980,7 +920,7 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
     // no more stages than K steps: a single-step conv (1x1, cin 64) needs one
     const int nsteps = a.ksteps / (BK / 64);
     // operand stages, enlarged to hold the staged output tile, + the residual tile (kernel layout)
-    constexpr bool TRT = !M32 && (WC % 4) == 0;
+    constexpr bool TRT = (WC % 4) == 0;
     constexpr int TILEB = L * BP * BC;
     const bool lines = BC >= 128 || BC == a.cout;
     int lds_bytes = (nsteps < NST ? nsteps : NST) * STAGE;
@@ -991,8 +931,8 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
     ConvArgs b = a;
     fast_div_init((int)nt, b.ntc_mul, b.ntc_shr);
     const bool lean = L >= 2 && a.yq && !a.y && !a.residual && !a.y_absmax;
-    auto kfull = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, false, PIPE, M32>;
-    auto klean = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, (L >= 2), PIPE, M32>;
+    auto kfull = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, false, PIPE>;
+    auto klean = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, (L >= 2), PIPE>;
     auto set_lds = [](const void* k) {
       const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                kMaxNeed < kMaxLds ? kMaxNeed : kMaxLds);
@@ -1049,14 +989,6 @@ static int launch_cfg(int cfg, const ConvArgs& a, hipStream_t s) {
     case 34: return launch_one<L, LW, 2, 2, 4, 2, false, 4, 2, 64, true>(a, s);
     case 35: return launch_one<L, LW, 1, 4, 4, 1, false, 4, 2, 64, true>(a, s);
     case 36: return launch_one<L, LW, 2, 2, 2, 2, false, 3, 2, 128, true>(a, s);
-    case 37: return launch_one<L, LW, 2, 2, 2, 1, false, 2, 2, 64, false, true>(a, s);
-    case 38: return launch_one<L, LW, 2, 2, 2, 1, false, 3, 2, 64, false, true>(a, s);
-    case 39: return launch_one<L, LW, 2, 2, 2, 1, false, 2, 2, 128, false, true>(a, s);
-    case 40: return launch_one<L, LW, 2, 2, 2, 1, false, 2, 2, 64, true, true>(a, s);
-    case 41: return launch_one<L, LW, 2, 2, 2, 1, false, 3, 2, 64, true, true>(a, s);
-    case 42: return launch_one<L, LW, 4, 1, 2, 1, false, 2, 2, 64, false, true>(a, s);
-    case 43: return launch_one<L, LW, 1, 4, 2, 1, false, 2, 2, 64, false, true>(a, s);
-    case 44: return launch_one<L, LW, 2, 2, 1, 2, false, 2, 2, 64, false, true>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   }
 }
