@@ -17,7 +17,7 @@ the timed steps cycle through all of them. Ranks calibrate together (engine.set_
 per-layer maxima are MAX-all-reduced), so the gathered logits equal a single-GPU forward of the
 global batch bit for bit. Prints ONE
 JSON line on rank 0 with the roofline of the dominant kernel family (the quantized conv:
-qconv_glds_kernel / qconv_kernel, every launch incl. the stem) and the CPU baseline (the
+qconv_glds_kernel and the fused stem + pool, every launch incl. the stem) and the CPU baseline (the
 reference's fp32 torch-CPU forward restated in oracle/torch_ref.py, timed on a bounded sample).
 
 Timing: `value` comes from the production path, the static-range forward replayed from a
@@ -31,6 +31,7 @@ that each event pair times one kernel alone). The roofline is SURVEY.md 8(d)'s: 
 T_roof = max(2 MACs / P_int8, bytes / BW_HBM) with ops/ops.alg_work's algorithmic bytes.
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -118,7 +119,7 @@ class ConvTimer:
         return {
             "bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": None,
-            "kernel": "quantized conv (qconv_glds_kernel + qconv_kernel), all launches incl. the stem",
+            "kernel": "quantized conv (qconv_glds_kernel + qconv_stem_pool_kernel), all launches incl. the stem",
             "launches_per_step": n // max(steps, 1),
             "avg_launch_ms": round(t_sum / max(n, 1) * 1e3, 5),
             "alg_bytes_per_launch": round(nbytes / max(n, 1)),
@@ -238,8 +239,10 @@ def main():
         engine.set_chunk(args.chunk)
     if args.streams:
         engine.STREAMS[0] = args.streams
-    if world > 1:
-        engine.set_dp_group(dist.group.WORLD)  # ranks calibrate together (MAX-all-reduced maxima)
+    # every step below runs on every rank in lockstep: the ranks calibrate together (MAX-all-reduced
+    # maxima) for as long as the block lasts (dp.lockstep scopes the engine's group to it)
+    lockstep = contextlib.ExitStack()
+    lockstep.enter_context(dp.lockstep())
     torch.manual_seed(0)
     net = getattr(resnet, arch)().to(dev).eval()
     assignments.apply_assignment(net, assign)
@@ -267,8 +270,8 @@ def main():
     for _ in range(max(1, args.warmup)):
         step()  # the first one calibrates on batch 0
     if rank == 0:
-        print("autotuned tiles:", {"x".join(map(str, k[:8])): v for k, v in ops._TUNED.items()},
-              file=sys.stderr, flush=True)
+        print("tiles (%s):" % json.dumps(ops.tile_table_info()),
+              {ops.key_str(k): v for k, v in ops._TUNED.items()}, file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -302,6 +305,7 @@ def main():
     timer.active = False
     ops.set_conv_hook(None)
     engine.USE_GRAPH[0], engine.CONCURRENT_DS[0], engine.STREAMS[0] = use_graph, conc, nst
+    lockstep.close()
     roof = timer.roofline(args.roofline_steps)
     if args.layers and rank == 0:
         timer.print_layers(args.roofline_steps)
@@ -338,7 +342,8 @@ def main():
                        "timed_calibrations": timed_stats["calibrations"],
                        "timed_overflow_reruns": timed_stats["overflow_reruns"],
                        "timed_stale_reruns": timed_stats["stale_reruns"],
-                       "timed_graph_captures": timed_stats["graph_captures"]},
+                       "timed_graph_captures": timed_stats["graph_captures"],
+                       "tile_table": ops.tile_table_info()},
             "roofline": roof,
         }
         if not args.no_cpu_baseline and world == 1:

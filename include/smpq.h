@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SMPQ_ABI_VERSION 3
+#define SMPQ_ABI_VERSION 4
 
 /* status codes */
 #define SMPQ_OK 0
@@ -110,8 +110,8 @@ int smpq_pack_weights(const float* w, int cout, int cin, int kh, int kw, const f
  *            channels that cannot be coded); 2 / 3: exact codes of quantized channels that fit
  *            16 / 24 bits, per-channel fixed point (max|w| / 32512 or / 8323072) for the others
  *            (status[2] counts them)
- *   cin      <= 4 (stem: channels padded to 4, K = ceil(kh*kw/16)*64) or a multiple of 64
- *            (K = kh*kw*cin, ordered [kh][kw][cin])
+ *   cin      a multiple of 64 (K = kh*kw*cin, ordered [kh][kw][cin]); the <= 4-channel stem is
+ *            packed by smpq_pack_weights_s2d_ex
  *   offset   device int32 [cout] (wlimbs == 1), wscale device fp32 [cout]: the per-channel weight
  *            step the codes are in (= step for exact channels)
  *   status   device int32 [3], caller-zeroed */
@@ -132,11 +132,6 @@ int smpq_act_absmax(const float* x, int n, int64_t per_image, float* absmax,
 int smpq_act_quantize(const float* x, int n, int64_t per_image, const float* absmax, int limbs,
                       int8_t* out, smpq_stream_t stream);
 
-/* Image batch NCHW fp32 [n][c][h][w] (c <= 4) -> `limbs` int8 planes NHWC with 4 channels
- * (zero padded): the stem conv's input (resnet.py:143). absmax from smpq_act_absmax. */
-int smpq_image_quantize(const float* x, int n, int c, int h, int w, const float* absmax, int limbs,
-                        int8_t* out, smpq_stream_t stream);
-
 /* MaxPool2d(3, stride 2, pad 1) (resnet.py:147) on NHWC fp32 [n][h][w][c] (c % 4 == 0), fused
  * with the activation quantizer of its output: `limbs` int8 planes [n][ho][wo][c] with the
  * per-image range absmax (the pool input's max; equal to the output's for ReLU outputs).
@@ -155,9 +150,11 @@ int smpq_maxpool_quantize(const float* x, int n, int h, int w, int c, const floa
  *   limbs      activation code width in int8 limbs: 1 (int8), 2 (int16), 3 (int24)
  *   y          device fp32 NHWC [n][ho][wo][cout]
  *   y_absmax   device fp32 [n] (caller-zeroed), receives max|y| per image, or NULL
- *   tile_cfg   block tile configuration (smpq_conv2d_tile_config), or -1 for the built-in choice:
- *              an SMPQ_TILE_LDS_DMA(_K128) configuration whenever one takes the shape; the
- *              register-staged family only for cin == 4 or planes of 2 GiB and more */
+ *   tile_cfg   block tile configuration (smpq_conv2d_tile_config), or -1 for the built-in choice
+ *   cout % 16 == 0, and every activation / output plane below 2 GiB (32-bit buffer offsets:
+ *   SMPQ_E_SHAPE otherwise; the Python layer splits such batches). ABI v4: the register-staged
+ *   kernel family of v1-v3 (and with it cin == 4) is gone; tile configurations are numbered from 0
+ *   in the LDS-DMA family. */
 int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                     const int8_t* codes, const int32_t* offset, int cout, int kh, int kw,
                     int stride, int pad, const float* col_scale, const float* col_shift,
@@ -165,9 +162,8 @@ int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w
                     int tile_cfg, smpq_stream_t stream);
 
 /* smpq_conv2d_fwd with weight limbs (1, 2, or 3 with limbs == 3): codes [wlimbs][cout][K] from
- * smpq_pack_weights_ex, and
- * cin == 4 (stem, K padded) supported besides cin % 64 == 0. col_scale must include the
- * per-channel weight step (wscale) of the packer. */
+ * smpq_pack_weights_ex. col_scale must include the per-channel weight step (wscale) of the
+ * packer. */
 int smpq_conv2d_fwd_ex(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                        const int8_t* codes, int wlimbs, const int32_t* offset, int cout, int kh,
                        int kw, int stride, int pad, const float* col_scale, const float* col_shift,
@@ -195,7 +191,7 @@ int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int
  * configurations then stage every weight piece from whole cache lines (the 64-B K slices of 16
  * consecutive output channels are one contiguous KiB) instead of 16 half lines — 6-21 % faster
  * on the MFMA-heavy convs. Results are bitwise those of smpq_conv2d_fwd_q. codes (row-major) is
- * still required: the register-staged configurations read it. codes_kmajor may be NULL. */
+ * still required (the v3 signature is kept); codes_kmajor may be NULL. */
 int smpq_conv2d_fwd_q_km(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                          const int8_t* codes, const int8_t* codes_kmajor, int wlimbs, const int32_t* offset,
                          int cout, int kh, int kw, int stride, int pad, const float* col_scale,
@@ -215,22 +211,25 @@ int smpq_maxpool_limbs(const int8_t* x, int n, int h, int w, int c, int limbs, i
 /* ---- space-to-depth stem (the 7x7 / stride 2 / pad 3 conv1 of resnet.py:143) -------------------
  * The stem runs as a 4x4 / stride 1 conv over 16-channel "space-to-depth" pixels (each a 2x2
  * block of the image with up to 4 channels), so every 64-byte K step of the int8 GEMM is one
- * tap row of whole 16-byte pixels. Results are bitwise identical to smpq_conv2d_fwd_q on the
- * 4-channel planes of smpq_image_quantize with the smpq_pack_weights_ex codes (same per-channel
- * fixed point, exact integer accumulation).
+ * tap row of whole 16-byte pixels (tests/test_gpu.py checks it against an exact emulation of the
+ * 7x7/2/3 conv on the quantized image).
  *
- * smpq_image_quantize_s2d: x fp32 NCHW [n][c <= 4][h][w], h and w even ->
- *   out int8 [limbs][n][h/2][w/2][16], channel (dy*2 + dx)*4 + ci = x[ci][2i + dy][2j + dx]
- *   quantized with the per-image absmax like smpq_image_quantize (zero for ci >= c).
- * smpq_pack_weights_s2d: w fp32 [cout][cin <= 4][7][7] -> codes int8 [wlimbs][cout][256] (K order
- *   [ty][tx][dy][dx][ci], original tap (2 ty + dy - 1, 2 tx + dx - 1), zero outside 7x7) in
- *   per-channel fixed point (wlimbs 2 / 3 = 16 / 24 bits) with scale wscale [cout];
- *   status[2] counts the channels coded. (No quantized-code mode: the stem is never quantized.)
+ * smpq_image_quantize_s2d: x fp32 NCHW [n][c <= 4][h][w] (h, w >= 2) ->
+ *   out int8 [limbs][n][ceil(h/2)][ceil(w/2)][16], channel (dy*2 + dx)*4 + ci = x[ci][2i + dy][2j + dx]
+ *   quantized with the per-image absmax as smpq_act_quantize does (zero for ci >= c and past an
+ *   odd h or w: the conv's own zero padding).
+ * smpq_pack_weights_s2d_ex: w fp32 [cout][cin <= 4][7][7] -> codes int8 [wlimbs][cout][256] (K order
+ *   [ty][tx][dy][dx][ci], original tap (2 ty + dy - 1, 2 tx + dx - 1), zero outside 7x7) with scale
+ *   wscale [cout]: channels with a recorded quantization step (step[c] > 0; step may be NULL) as
+ *   exact codes, the others in per-channel fixed point (wlimbs 2 / 3 = 16 / 24 bits) — the rules of
+ *   smpq_pack_weights_ex; status[3] as there. smpq_pack_weights_s2d = the same with step NULL.
  * smpq_stem_conv_s2d_q: as smpq_conv2d_fwd_q with the stem geometry (h, w = the ORIGINAL image
- *   size; output [n][h/2][w/2][cout] NHWC), no residual; cout % 16 == 0; tile_cfg one of the
- *   SMPQ_TILE_LDS_DMA configs with 64 output channels per block, or -1. */
+ *   size; output [n][ceil(h/2)][ceil(w/2)][cout] NHWC), no residual; cout % 16 == 0; tile_cfg one
+ *   of the tile configs with 64 output channels per block, or -1. */
 int smpq_image_quantize_s2d(const float* x, int n, int c, int h, int w, const float* absmax, int limbs,
                             int8_t* out, smpq_stream_t stream);
+int smpq_pack_weights_s2d_ex(const float* w, int cout, int cin, const float* step, int wlimbs, int8_t* codes,
+                             float* wscale, int32_t* status, smpq_stream_t stream);
 int smpq_pack_weights_s2d(const float* w, int cout, int cin, int wlimbs, int8_t* codes, float* wscale,
                           int32_t* status, smpq_stream_t stream);
 int smpq_stem_conv_s2d_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, const int8_t* codes,
@@ -267,14 +266,10 @@ int smpq_conv2d_num_tile_configs(void);
 int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads);
 
 /* Kernel family of a tile configuration:
- *   SMPQ_TILE_REGSTAGE         register-staged loader, cin % 64 == 0
- *   SMPQ_TILE_REGSTAGE_SMALLC  register-staged loader, also cin == 4 (the stem)
  *   SMPQ_TILE_LDS_DMA          LDS-DMA loader; cin % 64 == 0, cout % 16 == 0, every operand and
  *                              output plane < 2 GiB
  *   SMPQ_TILE_LDS_DMA_K128     as SMPQ_TILE_LDS_DMA with 128-wide K steps: also cin % 128 == 0
- * (negative: error code). */
-#define SMPQ_TILE_REGSTAGE 0
-#define SMPQ_TILE_REGSTAGE_SMALLC 1
+ * (negative: error code). Values 0 and 1 were the register-staged family (ABI <= 3, removed). */
 #define SMPQ_TILE_LDS_DMA 2
 #define SMPQ_TILE_LDS_DMA_K128 3
 int smpq_conv2d_tile_kind(int cfg);

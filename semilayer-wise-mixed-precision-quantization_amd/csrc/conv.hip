@@ -1,14 +1,15 @@
-// Quantized convolution forward for gfx950 (CDNA4): implicit GEMM on int8 MFMA.
+// Quantized convolution forward for gfx950 (CDNA4): the C-ABI of the int8-MFMA conv (its kernel,
+// qconv_glds_kernel, is in conv_glds_kernel.h) and the activation-side helper kernels
+// (quantizers, max pools, per-image ranges, the K-major weight copy).
 //
 // Replaces nn.Conv2d on the fake-quantized weight (resnet.py:22-30) together with the eval
 // BatchNorm, ReLU and residual add that follow it (resnet.py:55-68 / 97-116), and the
 // unquantized stem / downsample convs (resnet.py:143, 188-192).
 //
 // GEMM view (NHWC activations):
-//   M = n*ho*wo output pixels, N = cout, K = kh*kw*cin ordered [kh][kw][cin].
-//   * cin % 64 == 0: one 64-wide K step is 64 contiguous channels of one tap (64 B per limb).
-//   * cin == 4 (the stem: RGB padded to 4): one K step is 16 taps x 4 channels; K is padded
-//     with zero weights to a multiple of 64.
+//   M = n*ho*wo output pixels, N = cout, K = kh*kw*cin ordered [kh][kw][cin], cin % 64 == 0: one
+//   64-wide K step is 64 contiguous channels of one tap (64 B per limb). The 7x7/2 stem on <= 4
+//   channels runs as a 4x4/1 conv over 16-channel space-to-depth pixels (smpq_stem_conv_s2d_q).
 //   A[m][k] = activation code at the tap's input pixel (0 outside the image: zero padding).
 //   B[k][n] = weight code (int8 limbs, from smpq_pack_weights_ex).
 //
@@ -24,11 +25,6 @@
 // digits, weight <= 2^-22 of the top product, i.e. below the 24-bit quantization step itself) are
 // skipped: 6 passes instead of 9. All accumulation is exact integer arithmetic, so results are
 // independent of the tile configuration and of the batch composition (per-image steps).
-//
-// Tile: WAVES_M x WAVES_N waves; each wave owns WM x WN subtiles of 16 x 16 computed with
-// v_mfma_i32_16x16x64_i8. Global -> register prefetch of K step k+1 overlaps the MFMAs of step
-// k; one LDS double buffer, one barrier per K step; the epilogue reuses the LDS arena as an fp32
-// output tile so residual loads and output stores are whole 16-B pieces of contiguous rows.
 #include <algorithm>
 #include <climits>
 #include <cstdint>
@@ -38,472 +34,6 @@
 #include "conv_common.h"
 
 namespace smpq {
-
-constexpr int kRowBytes = 80;  // LDS row stride for a 64-byte K slice (+16 B pad vs conflicts)
-
-// Block = WAVES_M x WAVES_N waves; each wave owns WM x WN 16x16 subtiles.
-template <int L, int LW, bool SMALLC, int WAVES_M, int WAVES_N, int WM, int WN, int MINW, int PF>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, MINW) void qconv_kernel(ConvArgs a) {
-  constexpr int NT = 64 * WAVES_M * WAVES_N;
-  constexpr int BM = 16 * WM * WAVES_M;
-  constexpr int BN = 16 * WN * WAVES_N;
-  constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;  // lowest accumulated limb weight
-  constexpr int NACC = L + LW - 1 - SMIN;
-  constexpr int RPP = NT / 4;                  // 64-B rows covered per pass (4 threads per row)
-  constexpr int AR = (BM + RPP - 1) / RPP;     // A rows per thread per limb
-  constexpr int BROWS = (BN + RPP - 1) / RPP;  // B rows per thread per limb
-
-  // one LDS arena: K-loop operand buffers, then (after the loop) the fp32 output tile
-  constexpr int kABytes = 2 * L * BM * kRowBytes;
-  constexpr int kLoopBytes = kABytes + 2 * LW * BN * kRowBytes;
-  constexpr int TS = BN + 4;  // epilogue tile row stride (floats): conflict-free lane writes
-  constexpr int kEpiBytes = BM * TS * 4;
-  constexpr int kArena = kLoopBytes > kEpiBytes ? kLoopBytes : kEpiBytes;
-  __shared__ __attribute__((aligned(16))) int8_t arena[kArena];
-  typedef int8_t ATile[L][BM][kRowBytes];
-  typedef int8_t BTile[LW][BN][kRowBytes];
-  ATile* As = reinterpret_cast<ATile*>(arena);
-  BTile* Bs = reinterpret_cast<BTile*>(arena + kABytes);
-  float* tile = reinterpret_cast<float*>(arena);
-  __shared__ float s_rowscale[BM];
-  __shared__ int s_rowimg[BM];
-  __shared__ unsigned int s_rowmax[BM];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-
-  const int ntiles = (a.cout + BN - 1) / BN;
-  const int m0 = (blockIdx.x / ntiles) * BM;
-  const int n0 = (blockIdx.x % ntiles) * BN;
-  const int hw_out = a.ho * a.wo;
-
-  // ---- per-block row table: image index and activation step of each output row ----------
-  for (int r = tid; r < BM; r += NT) {
-    const int m = m0 + r;
-    int img = -1;
-    float sc = 0.f;
-    if (m < a.M) {
-      img = m / hw_out;
-      sc = a.x_absmax[img] * a.inv_qmax;
-    }
-    s_rowimg[r] = img;
-    s_rowscale[r] = sc;
-    s_rowmax[r] = 0u;
-  }
-
-  // ---- per-thread A load rows: input pixel base and top-left tap coordinate -----------------
-  const int piece = tid & 3;  // 16-B piece of a 64-B K slice
-  const int row0 = tid >> 2;  // rows row0 + RPP*i (A) / row0 + RPP*j (B)
-  int a_pix[AR];              // n*h*w pixel base, or -1 when the row is past M
-  int a_ih[AR], a_iw[AR];
-#pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const int m = m0 + row0 + RPP * i;
-    if (row0 + RPP * i < BM && m < a.M) {
-      const int img = m / hw_out;
-      const int rem = m - img * hw_out;
-      const int oh = rem / a.wo;
-      const int ow = rem - oh * a.wo;
-      a_pix[i] = img * a.h * a.w;
-      a_ih[i] = oh * a.stride - a.pad;
-      a_iw[i] = ow * a.stride - a.pad;
-    } else {
-      a_pix[i] = -1;
-      a_ih[i] = a_iw[i] = 0;
-    }
-  }
-
-  typedef v4i ASet[L][AR];
-  typedef v4i BSet[LW][BROWS];
-
-  auto load_global = [&](int ks, ASet& ra, BSet& rb) {
-    if constexpr (SMALLC) {
-      // 16 taps x 4 channels per K step; this thread's piece = taps 16*ks + 4*piece + 0..3
-      const int taps = a.kh * a.kw;
-#pragma unroll
-      for (int i = 0; i < AR; ++i) {
-        int v[L][4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int tap = 16 * ks + 4 * piece + t;
-          const int kr = tap / a.kw, kc = tap - (tap / a.kw) * a.kw;
-          const int ih = a_ih[i] + kr, iw = a_iw[i] + kc;
-          const bool ok = tap < taps && a_pix[i] >= 0 && (unsigned)ih < (unsigned)a.h &&
-                          (unsigned)iw < (unsigned)a.w;
-          const size_t off = ok ? (size_t)(a_pix[i] + ih * a.w + iw) * 4 : 0;
-#pragma unroll
-          for (int l = 0; l < L; ++l)
-            v[l][t] = ok ? *reinterpret_cast<const int*>(a.xq + l * a.plane + off) : 0;
-        }
-#pragma unroll
-        for (int l = 0; l < L; ++l) ra[l][i] = v4i{v[l][0], v[l][1], v[l][2], v[l][3]};
-      }
-    } else {
-      const int tap = ks / a.cchunks;
-      const int c0 = (ks - tap * a.cchunks) * kKStep;
-      const int kr = tap / a.kw;
-      const int kc = tap - kr * a.kw;
-#pragma unroll
-      for (int i = 0; i < AR; ++i) {
-        const int ih = a_ih[i] + kr;
-        const int iw = a_iw[i] + kc;
-        const bool ok = a_pix[i] >= 0 && (unsigned)ih < (unsigned)a.h && (unsigned)iw < (unsigned)a.w;
-        const size_t off = ok ? ((size_t)(a_pix[i] + ih * a.w + iw) * a.cin + c0 + 16 * piece) : 0;
-#pragma unroll
-        for (int l = 0; l < L; ++l) {
-          v4i v = {0, 0, 0, 0};
-          if (ok) v = *reinterpret_cast<const v4i*>(a.xq + l * a.plane + off);
-          ra[l][i] = v;
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < BROWS; ++j) {
-      const int col = n0 + row0 + RPP * j;
-      const bool ok = row0 + RPP * j < BN && col < a.cout;
-      const size_t off = ok ? (size_t)col * a.K + ks * kKStep + 16 * piece : 0;
-#pragma unroll
-      for (int lw = 0; lw < LW; ++lw) {
-        v4i v = {0, 0, 0, 0};
-        if (ok) v = *reinterpret_cast<const v4i*>(a.codes + lw * a.wplane + off);
-        rb[lw][j] = v;
-      }
-    }
-  };
-
-  auto store_lds = [&](int buf, const ASet& ra, const BSet& rb) {
-#pragma unroll
-    for (int l = 0; l < L; ++l)
-#pragma unroll
-      for (int i = 0; i < AR; ++i)
-        if (row0 + RPP * i < BM) *reinterpret_cast<v4i*>(&As[buf][l][row0 + RPP * i][16 * piece]) = ra[l][i];
-#pragma unroll
-    for (int lw = 0; lw < LW; ++lw)
-#pragma unroll
-      for (int j = 0; j < BROWS; ++j)
-        if (row0 + RPP * j < BN) *reinterpret_cast<v4i*>(&Bs[buf][lw][row0 + RPP * j][16 * piece]) = rb[lw][j];
-  };
-
-  v4i acc[NACC][WM][WN];
-  int rs[L][WM];  // per-lane partial row sums of A codes (LW == 1 offset correction)
-#pragma unroll
-  for (int s = 0; s < NACC; ++s)
-#pragma unroll
-    for (int i = 0; i < WM; ++i)
-#pragma unroll
-      for (int j = 0; j < WN; ++j) acc[s][i][j] = v4i{0, 0, 0, 0};
-#pragma unroll
-  for (int l = 0; l < L; ++l)
-#pragma unroll
-    for (int i = 0; i < WM; ++i) rs[l][i] = 0;
-
-  const int frow = lane & 15;       // fragment row/col owned by this lane
-  const int fk = 16 * (lane >> 4);  // fragment K byte offset owned by this lane
-  const int arow_base = wm * 16 * WM;
-  const int bcol_base = wn * 16 * WN;
-  const bool do_off = (LW == 1) && a.has_offset;
-
-  auto compute = [&](int buf) {
-    v4i bf[LW][WN];
-#pragma unroll
-    for (int lw = 0; lw < LW; ++lw)
-#pragma unroll
-      for (int j = 0; j < WN; ++j)
-        bf[lw][j] = *reinterpret_cast<const v4i*>(&Bs[buf][lw][bcol_base + 16 * j + frow][fk]);
-#pragma unroll
-    for (int l = 0; l < L; ++l) {
-#pragma unroll
-      for (int i = 0; i < WM; ++i) {
-        const v4i af = *reinterpret_cast<const v4i*>(&As[buf][l][arow_base + 16 * i + frow][fk]);
-        if (do_off) {
-          int s = rs[l][i];
-          s = __builtin_amdgcn_sdot4(af.x, 0x01010101, s, false);
-          s = __builtin_amdgcn_sdot4(af.y, 0x01010101, s, false);
-          s = __builtin_amdgcn_sdot4(af.z, 0x01010101, s, false);
-          s = __builtin_amdgcn_sdot4(af.w, 0x01010101, s, false);
-          rs[l][i] = s;
-        }
-#pragma unroll
-        for (int lw = 0; lw < LW; ++lw) {
-          if (l + lw < SMIN) continue;  // compile-time: skipped low-digit product
-#pragma unroll
-          for (int j = 0; j < WN; ++j)
-            acc[l + lw - SMIN][i][j] =
-                __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[lw][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
-        }
-      }
-    }
-  };
-
-  if constexpr (PF == 2) {
-  // K loop: two register staging sets, global loads issued two K steps ahead of their use
-  // (latency spans two MFMA phases), one LDS double buffer, one barrier per K step. Unrolled by
-  // two so every register set is statically indexed (no scratch).
-  ASet raA, raB;
-  BSet rbA, rbB;
-  load_global(0, raA, rbA);
-  store_lds(0, raA, rbA);
-  if (a.ksteps > 1) load_global(1, raB, rbB);
-  __syncthreads();
-  int ks = 0;
-  for (; ks + 1 < a.ksteps; ks += 2) {
-    if (ks + 2 < a.ksteps) load_global(ks + 2, raA, rbA);
-    compute(0);
-    store_lds(1, raB, rbB);
-    __syncthreads();
-    if (ks + 3 < a.ksteps) load_global(ks + 3, raB, rbB);
-    compute(1);
-    if (ks + 2 < a.ksteps) store_lds(0, raA, rbA);
-    __syncthreads();
-  }
-  if (ks < a.ksteps) compute(0);
-  } else {
-  // K loop: one register staging set, loads issued one K step ahead (fewer live registers:
-  // wins for the tiles with the most accumulators per wave)
-  ASet ra;
-  BSet rb;
-  load_global(0, ra, rb);
-  store_lds(0, ra, rb);
-  __syncthreads();
-  for (int ks = 0; ks < a.ksteps; ++ks) {
-    const int buf = ks & 1;
-    if (ks + 1 < a.ksteps) load_global(ks + 1, ra, rb);
-    compute(buf);
-    if (ks + 1 < a.ksteps) store_lds(buf ^ 1, ra, rb);
-    __syncthreads();
-  }
-  }
-
-  // ---- epilogue: recombine limbs, affine (dequant * BN), residual, ReLU, store, absmax ----
-  // row sums: lanes {l, l^16, l^32, l^48} hold the four K quarters of row (l & 15)
-  if (do_off) {
-#pragma unroll
-    for (int l = 0; l < L; ++l)
-#pragma unroll
-      for (int i = 0; i < WM; ++i) {
-        int s = rs[l][i];
-        s += __shfl_xor(s, 16, kWave);
-        s += __shfl_xor(s, 32, kWave);
-        rs[l][i] = s;
-      }
-  }
-
-  float colscale[WN], colshift[WN];
-  int coloff[WN];
-#pragma unroll
-  for (int j = 0; j < WN; ++j) {
-    const int col = n0 + bcol_base + 16 * j + frow;
-    const bool ok = col < a.cout;
-    colscale[j] = ok ? a.col_scale[col] : 0.f;
-    colshift[j] = ok ? a.col_shift[col] : 0.f;
-    coloff[j] = (ok && do_off) ? a.w_off[col] : 0;
-  }
-
-  // The K-loop buffers are dead: the arena becomes the [BM][TS] fp32 output tile. All global
-  // traffic of the epilogue is whole 16-B pieces of contiguous output rows (coalesced), and all
-  // residual loads are issued before any output store (vmcnt retires loads and stores in order).
-  constexpr int V4 = BN / 4;  // float4 per tile row
-  const bool vec_ok = (a.cout & 3) == 0;
-  __syncthreads();
-  if (a.res_q) {
-    // residual from the block input's int8 limb planes, 16 channels (16 B per limb) per item;
-    // every load of this thread is issued before the first use (constant trip count, unrolled)
-    constexpr int V16 = BN / 16;
-    constexpr int NIT = (BM * V16 + NT - 1) / NT;
-    const long long rplane = (long long)a.M * a.cout;
-    v4i rq[NIT][L];
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int e = tid + it * NT;
-      const int r = e / V16, c16 = e - (e / V16) * V16;
-      const int m = m0 + r, col = n0 + 16 * c16;
-      const bool ok = e < BM * V16 && m < a.M && col + 15 < a.cout;
-      const int8_t* src = a.res_q + (size_t)(ok ? m : 0) * a.cout + (ok ? col : 0);
-#pragma unroll
-      for (int l = 0; l < L; ++l) {
-        v4i v = {0, 0, 0, 0};
-        if (ok) v = *reinterpret_cast<const v4i*>(src + l * rplane);
-        rq[it][l] = v;
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int e = tid + it * NT;
-      if (e >= BM * V16) break;
-      const int r = e / V16, c16 = e - (e / V16) * V16;
-      const int m = m0 + r, col = n0 + 16 * c16;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {  // 4 channels per dword
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (m < a.M && col + 15 < a.cout) {
-          int q[4] = {0, 0, 0, 0};
-          int limbw = 1;
-#pragma unroll
-          for (int l = 0; l < L; ++l) {
-            const unsigned int wd = (unsigned int)rq[it][l][g];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) q[k] += (int)(int8_t)(wd >> (8 * k)) * limbw;
-            limbw *= 256;
-          }
-          v = make_float4(__fmul_rn(a.res_scale, (float)q[0]), __fmul_rn(a.res_scale, (float)q[1]),
-                          __fmul_rn(a.res_scale, (float)q[2]), __fmul_rn(a.res_scale, (float)q[3]));
-        } else if (m < a.M) {  // ragged channel tail (cout % 16 != 0): bytewise
-          const int8_t* src = a.res_q + (size_t)m * a.cout;
-          float t[4] = {0.f, 0.f, 0.f, 0.f};
-          for (int k = 0; k < 4; ++k) {
-            const int c = col + 4 * g + k;
-            if (c >= a.cout) break;
-            int q = 0, limbw = 1;
-            for (int l = 0; l < L; ++l) {
-              q += (int)src[l * rplane + c] * limbw;
-              limbw *= 256;
-            }
-            t[k] = __fmul_rn(a.res_scale, (float)q);
-          }
-          v = make_float4(t[0], t[1], t[2], t[3]);
-        }
-        *reinterpret_cast<float4*>(&tile[r * TS + 16 * c16 + 4 * g]) = v;
-      }
-    }
-    __syncthreads();
-  } else if (a.residual) {
-    for (int e = tid; e < BM * V4; e += NT) {
-      const int r = e / V4, c4 = e - (e / V4) * V4;
-      const int m = m0 + r, col = n0 + 4 * c4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (m < a.M) {
-        const float* src = a.residual + (size_t)m * a.cout + col;
-        if (vec_ok && col + 3 < a.cout) {
-          v = *reinterpret_cast<const float4*>(src);
-        } else {
-          if (col < a.cout) v.x = src[0];
-          if (col + 1 < a.cout) v.y = src[1];
-          if (col + 2 < a.cout) v.z = src[2];
-          if (col + 3 < a.cout) v.w = src[3];
-        }
-      }
-      *reinterpret_cast<float4*>(&tile[r * TS + 4 * c4]) = v;
-    }
-    __syncthreads();
-  }
-
-#pragma unroll
-  for (int i = 0; i < WM; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int rloc = arow_base + 16 * i + 4 * (lane >> 4) + r;  // C layout: row = 4*(lane>>4)+reg
-      const float rscale = s_rowscale[rloc];
-      int rsum[L];
-#pragma unroll
-      for (int l = 0; l < L; ++l) rsum[l] = do_off ? __shfl(rs[l][i], 4 * (lane >> 4) + r, kWave) : 0;
-      float rmax = 0.f;
-#pragma unroll
-      for (int j = 0; j < WN; ++j) {
-        const int cloc = bcol_base + 16 * j + frow;
-        float v = 0.f;
-        float limbw = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
-#pragma unroll
-        for (int s = 0; s < NACC; ++s) {
-          int t = acc[s][i][j][r];
-          if (SMIN == 0 && s < L) t += __mul24(coloff[j], rsum[s]);  // offsets only for LW == 1 (24-bit exact)
-          v = __fmaf_rn((float)t, limbw, v);
-          limbw *= 256.f;
-        }
-        float out = affine(v, rscale, colscale[j], colshift[j]);
-        float* tp = &tile[rloc * TS + cloc];
-        if (a.residual || a.res_q) out = __fadd_rn(out, *tp);
-        if (a.relu) out = fmaxf(out, 0.f);
-        *tp = out;
-        if (n0 + cloc < a.cout) rmax = fmaxf(rmax, fabsf(out));
-      }
-      if (a.y_absmax) {
-        // reduce over the 16 lanes (columns) that share this row
-        rmax = fmaxf(rmax, __shfl_xor(rmax, 1, kWave));
-        rmax = fmaxf(rmax, __shfl_xor(rmax, 2, kWave));
-        rmax = fmaxf(rmax, __shfl_xor(rmax, 4, kWave));
-        rmax = fmaxf(rmax, __shfl_xor(rmax, 8, kWave));
-        if (frow == 0 && m0 + rloc < a.M) atomicMax(&s_rowmax[rloc], __float_as_uint(rmax));
-      }
-    }
-  }
-  __syncthreads();
-  bool ovf = false;
-  if (a.y) {
-    for (int e = tid; e < BM * V4; e += NT) {
-      const int r = e / V4, c4 = e - (e / V4) * V4;
-      const int m = m0 + r, col = n0 + 4 * c4;
-      if (m >= a.M || col >= a.cout) continue;
-      const float4 v = *reinterpret_cast<const float4*>(&tile[r * TS + 4 * c4]);
-      float* dst = a.y + (size_t)m * a.cout + col;
-      if (vec_ok && col + 3 < a.cout) {
-        st16(dst, v4i{__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w)});
-      } else {
-        dst[0] = v.x;
-        if (col + 1 < a.cout) dst[1] = v.y;
-        if (col + 2 < a.cout) dst[2] = v.z;
-        if (col + 3 < a.cout) dst[3] = v.w;
-      }
-    }
-  }
-  if (a.yq) {
-    // fused activation quantizer of the NEXT conv's input (static per-layer range):
-    // 16 channels per item -> one 16-B store per limb plane
-    constexpr float qmax = act_qmax<L>();
-    constexpr int V16 = BN / 16;
-    const long long yplane = (long long)a.M * a.cout;
-    for (int e = tid; e < BM * V16; e += NT) {
-      const int r = e / V16, c16 = e - (e / V16) * V16;
-      const int m = m0 + r, col = n0 + 16 * c16;
-      if (m >= a.M || col >= a.cout) continue;
-      unsigned int word[L][4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 v = *reinterpret_cast<const float4*>(&tile[r * TS + 16 * c16 + 4 * g]);
-        const float vals[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int l = 0; l < L; ++l) word[l][g] = 0u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float qf = rintf(__fmul_rn(vals[k], a.yq_inv));
-          ovf |= (col + 4 * g + k < a.cout) && fabsf(qf) > qmax;
-          qf = fminf(fmaxf(qf, -qmax), qmax);
-          int d[L];
-          split_limbs<L>((int)qf, d);
-#pragma unroll
-          for (int l = 0; l < L; ++l) word[l][g] |= (unsigned int)(d[l] & 255) << (8 * k);
-        }
-      }
-      int8_t* dq = a.yq + (size_t)m * a.cout + col;
-      if (col + 15 < a.cout) {
-#pragma unroll
-        for (int l = 0; l < L; ++l)
-          st16(dq + l * yplane, v4i{(int)word[l][0], (int)word[l][1], (int)word[l][2], (int)word[l][3]});
-      } else {
-        for (int l = 0; l < L; ++l)
-          for (int k = 0; k < 16 && col + k < a.cout; ++k)
-            dq[l * yplane + k] = (int8_t)(word[l][k >> 2] >> (8 * (k & 3)));
-      }
-    }
-  }
-  if (a.yq && __any(ovf) && lane == 0) atomicMax(a.overflow, 1);
-
-  if (a.y_absmax) {
-    if (wave == 0) {
-      const int img_lo = s_rowimg[0];
-      const int last = min(BM, a.M - m0) - 1;
-      const int img_hi = s_rowimg[last];
-      for (int img = img_lo; img <= img_hi; ++img) {
-        float v = 0.f;
-        for (int r = lane; r < BM; r += kWave)
-          if (s_rowimg[r] == img) v = fmaxf(v, __uint_as_float(s_rowmax[r]));
-        v = wave_max(v);
-        if (lane == 0 && v > 0.f) atomic_max_nonneg(&a.y_absmax[img], v);
-      }
-    }
-  }
-}
 
 // ------------------------------------------------------------------------------------------
 // x (fp32, any layout, n images of per_image elements) -> L int8 digit planes of
@@ -547,45 +77,18 @@ __global__ __launch_bounds__(256) void act_quantize_kernel(const float* __restri
   }
 }
 
-// NCHW fp32 image batch (c <= 4 channels) -> L int8 limb planes, NHWC with 4 channels (zero pad).
-template <int L>
-__global__ __launch_bounds__(256) void image_quantize_kernel(const float* __restrict__ x, int n, int c,
-                                                             int hw, const float* __restrict__ absmax,
-                                                             int8_t* __restrict__ out, long long plane) {
-  const float qmax = act_qmax<L>();
-  const long long total = (long long)n * hw;
-  for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < total;
-       p += (long long)gridDim.x * blockDim.x) {
-    const int img = (int)(p / hw);
-    const int pix = (int)(p - (long long)img * hw);
-    const float am = absmax[img];
-    const float inv = am > 0.f ? qmax / am : 0.f;
-    unsigned int word[L];
-#pragma unroll
-    for (int l = 0; l < L; ++l) word[l] = 0u;
-    for (int ch = 0; ch < c; ++ch) {
-      const float v = x[((size_t)img * c + ch) * hw + pix];
-      float qf = fminf(fmaxf(rintf(v * inv), -qmax), qmax);
-      int d[L];
-      split_limbs<L>((int)qf, d);
-#pragma unroll
-      for (int l = 0; l < L; ++l) word[l] |= (unsigned int)(d[l] & 255) << (8 * ch);
-    }
-#pragma unroll
-    for (int l = 0; l < L; ++l) *reinterpret_cast<unsigned int*>(out + l * plane + 4 * p) = word[l];
-  }
-}
-
-// NCHW fp32 images (c <= 4 channels, even h and w) -> L int8 limb planes in space-to-depth
-// layout [n][h/2][w/2][16], channel (dy * 2 + dx) * 4 + c = pixel (2i + dy, 2j + dx), channel c
-// (zero for c >= c_in): the stem's 7x7/2 conv becomes a 4x4/1 conv over 16-channel pixels whose
-// 64-B K steps are whole tap rows (smpq_stem_conv_s2d_q). One thread = one 16-channel pixel.
+// NCHW fp32 images (c <= 4 channels) -> L int8 limb planes in space-to-depth layout
+// [n][ceil(h/2)][ceil(w/2)][16], channel (dy * 2 + dx) * 4 + c = pixel (2i + dy, 2j + dx), channel c
+// (zero for c >= c_in, and for a pixel past an odd h or w: the stem conv's own zero padding): the
+// stem's 7x7/2 conv becomes a 4x4/1 conv over 16-channel pixels whose 64-B K steps are whole tap
+// rows (smpq_stem_conv_s2d_q). One thread = one 16-channel pixel.
 template <int L>
 __global__ __launch_bounds__(256) void image_quantize_s2d_kernel(const float* __restrict__ x, int n, int c, int h,
                                                                  int w, const float* __restrict__ absmax,
                                                                  int8_t* __restrict__ out, long long plane) {
   const float qmax = act_qmax<L>();
-  const int h2 = h / 2, w2 = w / 2;
+  const int h2 = (h + 1) / 2, w2 = (w + 1) / 2;
+  const bool even_w = (w & 1) == 0;
   const long long total = (long long)n * h2 * w2;
   for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < total;
        p += (long long)gridDim.x * blockDim.x) {
@@ -603,8 +106,17 @@ __global__ __launch_bounds__(256) void image_quantize_s2d_kernel(const float* __
     for (int ch = 0; ch < c; ++ch) {
 #pragma unroll
       for (int dy = 0; dy < 2; ++dy) {
-        const float2 v = *reinterpret_cast<const float2*>(x + (((size_t)img * c + ch) * h + 2 * i + dy) * w + 2 * j);
-        const float vals[2] = {v.x, v.y};
+        if (2 * i + dy >= h) continue;  // odd h: the zero row
+        const float* row = x + (((size_t)img * c + ch) * h + 2 * i + dy) * w + 2 * j;
+        float vals[2];
+        if (even_w) {
+          const float2 v = *reinterpret_cast<const float2*>(row);
+          vals[0] = v.x;
+          vals[1] = v.y;
+        } else {  // odd w: rows are not 8-B aligned, and the last column pair has one pixel
+          vals[0] = row[0];
+          vals[1] = 2 * j + 1 < w ? row[1] : 0.f;
+        }
 #pragma unroll
         for (int dx = 0; dx < 2; ++dx) {
           const float qf = fminf(fmaxf(rintf(vals[dx] * inv), -qmax), qmax);
@@ -770,93 +282,6 @@ __global__ void debug_mfma_kernel(const int8_t* a, const int8_t* b, int32_t* c) 
   for (int r = 0; r < 4; ++r) c[(4 * (lane >> 4) + r) * 16 + frow] = acc[r];
 }
 
-// ------------------------------------------------------------------------------------------
-template <int L, int LW, bool SMALLC, int WAVES_M, int WAVES_N, int WM, int WN, int MINW, int PF>
-static int launch(const ConvArgs& a, hipStream_t stream) {
-  constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
-  if constexpr ((L + LW - 1 - SMIN) * WM * WN * 4 > 128) {
-    // more than 128 accumulator registers per lane: not instantiated (would spill)
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: tile config too large for these limb counts");
-  } else {
-    constexpr int BM = 16 * WM * WAVES_M, BN = 16 * WN * WAVES_N;
-    const long mt = (a.M + BM - 1) / BM;
-    const long nt = (a.cout + BN - 1) / BN;
-    const long blocks = mt * nt;
-    if (blocks > 0x7fffffffL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
-    hipLaunchKernelGGL((qconv_kernel<L, LW, SMALLC, WAVES_M, WAVES_N, WM, WN, MINW, PF>), dim3((unsigned)blocks),
-                       dim3(64 * WAVES_M * WAVES_N), 0, stream, a);
-    return check_hip(hipGetLastError(), "qconv_kernel launch");
-  }
-}
-
-// Tile configurations: {waves_m, waves_n, wm, wn} -> BM x BN block tile, 64*waves threads.
-struct TileCfg {
-  int wavesm, wavesn, wm, wn;
-};
-constexpr TileCfg kTileCfgs[] = {
-    {2, 2, 4, 4},  // 0: 128 x 128, 256 threads
-    {2, 2, 2, 4},  // 1:  64 x 128, 256 threads
-    {2, 2, 4, 2},  // 2: 128 x  64, 256 threads
-    {2, 2, 2, 2},  // 3:  64 x  64, 256 threads
-    {2, 4, 4, 2},  // 4: 128 x 128, 512 threads (waves 64 x 32)
-    {4, 2, 2, 4},  // 5: 128 x 128, 512 threads (waves 32 x 64)
-};
-constexpr int kNumBaseCfgs = sizeof(kTileCfgs) / sizeof(kTileCfgs[0]);
-// Configs [0, 6) stage global loads two K steps ahead, [6, 12) are the same tiles with one step
-// of prefetch (fewer live registers). Neither wins everywhere; the host autotuner picks.
-constexpr int kNumTileCfgs = 2 * kNumBaseCfgs;
-
-template <int L, int LW, int PF>
-static int launch_cfg(int cfg, bool smallc, const ConvArgs& a, hipStream_t s) {
-  if (smallc) {
-    if constexpr (LW >= 2 && L >= 2) {
-      switch (cfg) {
-        case 2: return launch<L, LW, true, 2, 2, 4, 2, 2, PF>(a, s);
-        case 3: return launch<L, LW, true, 2, 2, 2, 2, 4, PF>(a, s);
-        default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: cin==4 supports tile configs 2, 3");
-      }
-    } else {
-      return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: cin==4 needs 2 weight limbs and >= 2 activation limbs");
-    }
-  }
-  switch (cfg) {
-    case 0: return launch<L, LW, false, 2, 2, 4, 4, 2, PF>(a, s);
-    case 1: return launch<L, LW, false, 2, 2, 2, 4, 2, PF>(a, s);
-    case 2: return launch<L, LW, false, 2, 2, 4, 2, 2, PF>(a, s);
-    case 3: return launch<L, LW, false, 2, 2, 2, 2, 4, PF>(a, s);
-    case 4: return launch<L, LW, false, 2, 4, 4, 2, 2, PF>(a, s);
-    case 5: return launch<L, LW, false, 4, 2, 2, 4, 2, PF>(a, s);
-    default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
-  }
-}
-
-template <int PF>
-static int dispatch_limbs(int cfg, bool smallc, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s) {
-  if (wlimbs == 1) {
-    switch (limbs) {
-      case 1: return launch_cfg<1, 1, PF>(cfg, smallc, a, s);
-      case 2: return launch_cfg<2, 1, PF>(cfg, smallc, a, s);
-      default: return launch_cfg<3, 1, PF>(cfg, smallc, a, s);
-    }
-  }
-  if (wlimbs == 3) return launch_cfg<3, 3, PF>(cfg, smallc, a, s);
-  switch (limbs) {
-    case 1: return launch_cfg<1, 2, PF>(cfg, smallc, a, s);
-    case 2: return launch_cfg<2, 2, PF>(cfg, smallc, a, s);
-    default: return launch_cfg<3, 2, PF>(cfg, smallc, a, s);
-  }
-}
-
-// Default tile when the caller does not pass one (the Python layer autotunes per shape).
-static int heuristic_cfg(int nacc, long M, int cout, int K, bool smallc) {
-  if (nacc >= 4) return 3;  // (accumulator sets after skipping; see SMIN)
-  if (smallc) return 2;
-  if (cout <= 64) return M >= 128L * 512 ? 2 : 3;
-  if (nacc >= 3) return 3;
-  if (K <= 256) return 1;
-  return 5;
-}
-
 }  // namespace smpq
 
 using namespace smpq;
@@ -877,10 +302,10 @@ static int conv_args_q(const int8_t* xq, const float* x_absmax, int n, int h, in
   if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || stride <= 0 ||
       pad < 0)
     return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: bad shape");
-  const bool smallc = cin == 4;
-  if (!smallc && cin % kKStep != 0)
-    return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: cin must be 4 or a multiple of 64 (got " +
-                                  std::to_string(cin) + ")");
+  if (cin % kKStep != 0)
+    return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: cin must be a multiple of 64 (got " + std::to_string(cin) +
+                                  "; the <= 4-channel 7x7/2 stem runs on smpq_stem_conv_s2d_q)");
+  if (cout % 16 != 0) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: cout must be a multiple of 16");
   if (wlimbs < 1 || wlimbs > 3) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: wlimbs must be 1, 2 or 3");
   if (wlimbs == 3 && limbs != 3)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: 3 weight limbs are built for 3 activation limbs only");
@@ -917,16 +342,9 @@ static int conv_args_q(const int8_t* xq, const float* x_absmax, int n, int h, in
   if (M > 0x7fffffffL || a.plane > 0x7fffffffLL * 8 || (long)n * h * w > 0x7fffffffL)
     return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: tensor too large");
   a.M = (int)M;
-  if (smallc) {
-    const int taps = kh * kw;
-    a.ksteps = (taps + 15) / 16;
-    a.K = a.ksteps * kKStep;
-    a.cchunks = 1;
-  } else {
-    a.K = kh * kw * cin;
-    a.cchunks = cin / kKStep;
-    a.ksteps = kh * kw * a.cchunks;
-  }
+  a.K = kh * kw * cin;
+  a.cchunks = cin / kKStep;
+  a.ksteps = kh * kw * a.cchunks;
   a.wplane = (long long)cout * a.K;
   a.relu = relu ? 1 : 0;
   a.has_offset = (offset && wlimbs == 1) ? 1 : 0;
@@ -957,32 +375,19 @@ extern "C" int smpq_conv2d_fwd_q_km(const int8_t* xq, const float* x_absmax, int
                              col_shift, residual, relu, limbs, y, y_absmax, yq, yq_range, overflow, residual_q,
                              residual_range, a);
   if (rc) return rc;
-  const bool smallc = cin == 4;
-  const long M = a.M;
-  hipStream_t s = (hipStream_t)stream;
   if (tile_cfg < 0) {
-    // the LDS-DMA family whenever it takes the shape; the register-staged family only where it
-    // cannot (cin == 4, planes >= 2 GiB): that kernel showed a rare, unexplained limb-plane
-    // mismatch under the repeated-launch screen, so no default reaches it otherwise
-    const int g = glds_default_cfg(a, limbs, wlimbs);
-    if (g >= 0) {
-      tile_cfg = kNumTileCfgs + g;
-    } else {
-      const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
-      tile_cfg = heuristic_cfg(limbs + wlimbs - 1 - smin, M, cout, a.K, smallc);
-    }
+    tile_cfg = glds_default_cfg(a, limbs, wlimbs);
+    // every operand and output plane is addressed with 32-bit buffer offsets: larger batches are
+    // split by the caller (smpq.ops.conv2d_q chunks the images)
+    if (tile_cfg < 0)
+      return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: a limb plane of 2 GiB or more (split the batch)");
   }
-  if (tile_cfg >= kNumTileCfgs + glds_num_cfgs()) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
-  if (tile_cfg >= kNumTileCfgs) {
-    if (smallc) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: LDS-DMA tile configs need cin % 64 == 0");
-    if (codes_kmajor) {  // the same codes, K-major (smpq_weights_kmajor): whole-line weight DMA pieces
-      a.codes = codes_kmajor;
-      a.w_kmajor = 1;
-    }
-    return launch_glds(tile_cfg - kNumTileCfgs, limbs, wlimbs, a, s);
+  if (tile_cfg >= glds_num_cfgs()) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
+  if (codes_kmajor) {  // the same codes, K-major (smpq_weights_kmajor): whole-line weight DMA pieces
+    a.codes = codes_kmajor;
+    a.w_kmajor = 1;
   }
-  if (tile_cfg >= kNumBaseCfgs) return dispatch_limbs<1>(tile_cfg - kNumBaseCfgs, smallc, limbs, wlimbs, a, s);
-  return dispatch_limbs<2>(tile_cfg, smallc, limbs, wlimbs, a, s);
+  return launch_glds(tile_cfg, limbs, wlimbs, a, (hipStream_t)stream);
 }
 
 extern "C" int smpq_conv2d_fwd_q(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
@@ -1044,43 +449,22 @@ extern "C" int smpq_conv2d_fwd(const int8_t* xq, const float* x_absmax, int n, i
                             col_scale, col_shift, residual, relu, limbs, y, y_absmax, tile_cfg, stream);
 }
 
-extern "C" int smpq_conv2d_num_tile_configs(void) { return kNumTileCfgs + glds_num_cfgs(); }
+extern "C" int smpq_conv2d_num_tile_configs(void) { return glds_num_cfgs(); }
 
 extern "C" int smpq_conv2d_tile_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs) {
-  if (cfg < 0 || cfg >= kNumTileCfgs + glds_num_cfgs() || limbs < 1 || limbs > 3 || wlimbs < 1 || wlimbs > 3)
-    return 0;
-  if (cfg >= kNumTileCfgs) return glds_supported(cfg - kNumTileCfgs, cin, cout, kh, kw, limbs, wlimbs) ? 1 : 0;
-  const TileCfg& t = kTileCfgs[cfg % kNumBaseCfgs];
-  const int b = cfg % kNumBaseCfgs;
-  if (cin == 4) {
-    if (!(b == 2 || b == 3) || wlimbs < 2 || limbs < 2) return 0;
-  } else if (cin % kKStep != 0) {
-    return 0;
-  }
-  if (wlimbs == 3 && limbs != 3) return 0;
-  const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
-  return (limbs + wlimbs - 1 - smin) * t.wm * t.wn * 4 <= 128 ? 1 : 0;
+  if (cfg < 0 || cfg >= glds_num_cfgs() || limbs < 1 || limbs > 3 || wlimbs < 1 || wlimbs > 3) return 0;
+  return glds_supported(cfg, cin, cout, kh, kw, limbs, wlimbs) ? 1 : 0;
 }
 
 extern "C" int smpq_conv2d_tile_kind(int cfg) {
-  if (cfg < 0 || cfg >= kNumTileCfgs + glds_num_cfgs())
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_tile_kind: bad config");
-  if (cfg >= kNumTileCfgs) return glds_cfg_bk(cfg - kNumTileCfgs) == 128 ? SMPQ_TILE_LDS_DMA_K128 : SMPQ_TILE_LDS_DMA;
-  const int b = cfg % kNumBaseCfgs;
-  return (b == 2 || b == 3) ? SMPQ_TILE_REGSTAGE_SMALLC : SMPQ_TILE_REGSTAGE;
+  if (cfg < 0 || cfg >= glds_num_cfgs()) return fail(SMPQ_E_INVALID, "smpq_conv2d_tile_kind: bad config");
+  return glds_cfg_bk(cfg) == 128 ? SMPQ_TILE_LDS_DMA_K128 : SMPQ_TILE_LDS_DMA;
 }
 
 extern "C" int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads) {
-  if (cfg < 0 || cfg >= kNumTileCfgs + glds_num_cfgs() || !bm || !bn || !threads)
+  if (cfg < 0 || cfg >= glds_num_cfgs() || !bm || !bn || !threads)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_tile_config: bad arguments");
-  if (cfg >= kNumTileCfgs) {
-    glds_cfg_info(cfg - kNumTileCfgs, bm, bn, threads);
-    return SMPQ_OK;
-  }
-  const TileCfg& t = kTileCfgs[cfg % kNumBaseCfgs];
-  *bm = 16 * t.wm * t.wavesm;
-  *bn = 16 * t.wn * t.wavesn;
-  *threads = 64 * t.wavesm * t.wavesn;
+  glds_cfg_info(cfg, bm, bn, threads);
   return SMPQ_OK;
 }
 
@@ -1112,28 +496,11 @@ extern "C" int smpq_act_quantize(const float* x, int n, int64_t per_image, const
   return check_hip(hipGetLastError(), "act_quantize_kernel launch");
 }
 
-extern "C" int smpq_image_quantize(const float* x, int n, int c, int h, int w, const float* absmax, int limbs,
-                                   int8_t* out, smpq_stream_t stream) {
-  if (!x || !absmax || !out || n <= 0 || c <= 0 || c > 4 || h <= 0 || w <= 0)
-    return fail(SMPQ_E_INVALID, "smpq_image_quantize: bad arguments");
-  const long long hw = (long long)h * w;
-  const long long plane = (long long)n * hw * 4;
-  const dim3 grid((unsigned)grid_for((long long)n * hw));
-  hipStream_t s = (hipStream_t)stream;
-  switch (limbs) {
-    case 1: hipLaunchKernelGGL(image_quantize_kernel<1>, grid, dim3(256), 0, s, x, n, c, (int)hw, absmax, out, plane); break;
-    case 2: hipLaunchKernelGGL(image_quantize_kernel<2>, grid, dim3(256), 0, s, x, n, c, (int)hw, absmax, out, plane); break;
-    case 3: hipLaunchKernelGGL(image_quantize_kernel<3>, grid, dim3(256), 0, s, x, n, c, (int)hw, absmax, out, plane); break;
-    default: return fail(SMPQ_E_INVALID, "smpq_image_quantize: limbs must be 1, 2 or 3");
-  }
-  return check_hip(hipGetLastError(), "image_quantize_kernel launch");
-}
-
 extern "C" int smpq_image_quantize_s2d(const float* x, int n, int c, int h, int w, const float* absmax, int limbs,
                                        int8_t* out, smpq_stream_t stream) {
-  if (!x || !absmax || !out || n <= 0 || c <= 0 || c > 4 || h <= 1 || w <= 1 || (h & 1) || (w & 1))
-    return fail(SMPQ_E_INVALID, "smpq_image_quantize_s2d: need 1..4 channels and even h, w");
-  const long long total = (long long)n * (h / 2) * (w / 2);
+  if (!x || !absmax || !out || n <= 0 || c <= 0 || c > 4 || h <= 1 || w <= 1)
+    return fail(SMPQ_E_INVALID, "smpq_image_quantize_s2d: need 1..4 channels and h, w >= 2");
+  const long long total = (long long)n * ((h + 1) / 2) * ((w + 1) / 2);
   const long long plane = total * 16;
   const dim3 grid((unsigned)std::min<long long>((total + 255) / 256, 65535));
   hipStream_t s = (hipStream_t)stream;
@@ -1155,12 +522,11 @@ extern "C" int smpq_stem_conv_s2d_q(const int8_t* xq, const float* x_absmax, int
     return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: null pointer");
   if (yq && (!overflow || !(yq_range > 0.f)))
     return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: yq needs overflow flag and a positive range");
-  if (n <= 0 || h <= 1 || w <= 1 || (h & 1) || (w & 1) || cout <= 0)
-    return fail(SMPQ_E_SHAPE, "smpq_stem_conv_s2d_q: bad shape (h, w must be even)");
+  if (n <= 0 || h <= 1 || w <= 1 || cout <= 0 || cout % 16 != 0)
+    return fail(SMPQ_E_SHAPE, "smpq_stem_conv_s2d_q: bad shape (h, w >= 2, cout % 16 == 0)");
   if (limbs < 1 || limbs > 3) return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: limbs must be 1, 2 or 3");
-  if (tile_cfg < 0) tile_cfg = kNumTileCfgs;  // LDS-DMA 64 x 64
-  if (tile_cfg < kNumTileCfgs || tile_cfg >= kNumTileCfgs + glds_num_cfgs())
-    return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: the stem runs on the LDS-DMA tile configs");
+  if (tile_cfg < 0) tile_cfg = 0;  // 64 x 64
+  if (tile_cfg >= glds_num_cfgs()) return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: bad tile config");
   ConvArgs a = {};
   a.s2d = 1;
   a.xq = xq;
@@ -1174,8 +540,10 @@ extern "C" int smpq_stem_conv_s2d_q(const int8_t* xq, const float* x_absmax, int
   a.overflow = overflow;
   a.yq_inv = yq ? (limbs == 1 ? 127.f : (limbs == 2 ? 32512.f : 8323072.f)) / yq_range : 0.f;
   a.n = n;
-  a.h = h / 2;  // space-to-depth geometry: 4x4 taps, stride 1, pad 2 (top / left; bottom / right by range)
-  a.w = w / 2;
+  // space-to-depth geometry: 4x4 taps, stride 1, pad 2 (top / left; bottom / right by range). An odd
+  // h or w gets a zero row / column from smpq_image_quantize_s2d: the conv's own zero padding there
+  a.h = (h + 1) / 2;
+  a.w = (w + 1) / 2;
   a.cin = 16;
   a.cout = cout;
   a.kh = a.kw = 4;
@@ -1194,7 +562,7 @@ extern "C" int smpq_stem_conv_s2d_q(const int8_t* xq, const float* x_absmax, int
   fast_div_init(a.ho * a.wo, a.hw_mul, a.hw_shr);
   fast_div_init(a.wo, a.wo_mul, a.wo_shr);
   if ((long long)n * a.ho * a.wo > 0x7fffffffLL) return fail(SMPQ_E_SHAPE, "smpq_stem_conv_s2d_q: tensor too large");
-  return launch_glds(tile_cfg - kNumTileCfgs, limbs, wlimbs, a, (hipStream_t)stream);
+  return launch_glds(tile_cfg, limbs, wlimbs, a, (hipStream_t)stream);
 }
 
 extern "C" int smpq_maxpool_quantize(const float* x, int n, int h, int w, int c, const float* absmax, int limbs,

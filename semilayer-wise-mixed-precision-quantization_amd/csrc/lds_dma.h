@@ -130,19 +130,15 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // LDS-DMA kernels use it, so their static-range outputs agree bit for bit.
 // lean_codes: the same, returning the clamped codes themselves (the fused stem + max pool pools
 // them before encoding).
-template <int L, int NACC, int SMIN>
-__device__ __forceinline__ float lean_codes(const v4i* accs, float rscale, const float* csq, const float* shq,
-                                            bool has_res, const int* rqv, float rsq, bool relu, float lo, int* q) {
+// lean_codes_v: the same from the recombined v (the limb-outer K loop folds its limbs itself).
+template <int L>
+__device__ __forceinline__ float lean_codes_v(const float* vs, float rscale, const float* csq, const float* shq,
+                                              bool has_res, const int* rqv, float rsq, bool relu, float lo, int* q) {
   constexpr float qmax = act_qmax<L>();
-  constexpr float w0 = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
   float m = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    float v = (float)accs[0][r];
-    if (SMIN != 0) v = v * w0;
-#pragma unroll
-    for (int t = 1; t < NACC; ++t) v = __fmaf_rn((float)accs[t][r], w0 * (float)(1 << (8 * t)), v);
-    float z = __fmaf_rn(v, rscale * csq[r], shq[r]);
+    float z = __fmaf_rn(vs[r], rscale * csq[r], shq[r]);
     if (has_res) z = __fmaf_rn((float)rqv[r], rsq, z);
     const float zr = rintf(z);
     m = fmaxf(m, relu ? zr : fabsf(zr));
@@ -152,11 +148,37 @@ __device__ __forceinline__ float lean_codes(const v4i* accs, float rscale, const
 }
 
 template <int L, int NACC, int SMIN>
+__device__ __forceinline__ float lean_codes(const v4i* accs, float rscale, const float* csq, const float* shq,
+                                            bool has_res, const int* rqv, float rsq, bool relu, float lo, int* q) {
+  constexpr float w0 = SMIN == 0 ? 1.f : (SMIN == 1 ? 256.f : 65536.f);
+  float vs[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = (float)accs[0][r];
+    if (SMIN != 0) v = v * w0;
+#pragma unroll
+    for (int t = 1; t < NACC; ++t) v = __fmaf_rn((float)accs[t][r], w0 * (float)(1 << (8 * t)), v);
+    vs[r] = v;
+  }
+  return lean_codes_v<L>(vs, rscale, csq, shq, has_res, rqv, rsq, relu, lo, q);
+}
+
+template <int L, int NACC, int SMIN>
 __device__ __forceinline__ float lean_quad(const v4i* accs, float rscale, const float* csq, const float* shq,
                                            bool has_res, const int* rqv, float rsq, bool relu, float lo,
                                            unsigned* wq) {
   int q[4];
   const float m = lean_codes<L, NACC, SMIN>(accs, rscale, csq, shq, has_res, rqv, rsq, relu, lo, q);
+  encode4<L>(q, wq);
+  return m;
+}
+
+template <int L>
+__device__ __forceinline__ float lean_quad_v(const float* vs, float rscale, const float* csq, const float* shq,
+                                             bool has_res, const int* rqv, float rsq, bool relu, float lo,
+                                             unsigned* wq) {
+  int q[4];
+  const float m = lean_codes_v<L>(vs, rscale, csq, shq, has_res, rqv, rsq, relu, lo, q);
   encode4<L>(q, wq);
   return m;
 }

@@ -295,30 +295,28 @@ extern "C" int smpq_pack_weights_ex(const float* w, int cout, int cin, int kh, i
   if (wlimbs < 1 || wlimbs > 3) return fail(SMPQ_E_INVALID, "smpq_pack_weights_ex: wlimbs must be 1, 2 or 3");
   if (wlimbs == 1 && (!step || !offset))
     return fail(SMPQ_E_INVALID, "smpq_pack_weights_ex: wlimbs == 1 needs step and offset");
-  int cin_pad, K;
-  if (cin <= 4) {
-    cin_pad = 4;
-    K = ((kh * kw + 15) / 16) * 64;
-  } else if (cin % 64 == 0) {
-    cin_pad = cin;
-    K = cin * kh * kw;
-  } else {
-    return fail(SMPQ_E_SHAPE, "smpq_pack_weights_ex: cin must be <= 4 or a multiple of 64");
-  }
+  if (cin % 64 != 0)
+    return fail(SMPQ_E_SHAPE,
+                "smpq_pack_weights_ex: cin must be a multiple of 64 (the <= 4-channel stem: smpq_pack_weights_s2d_ex)");
+  const int K = cin * kh * kw;
   hipLaunchKernelGGL(pack_weights_ex_kernel, dim3(cout), dim3(kQThreads), 0, (hipStream_t)stream, w,
-                     cin, kh, kw, cin_pad, K, wlimbs, 0, step, codes, (long long)cout * K, offset, wscale,
+                     cin, kh, kw, cin, K, wlimbs, 0, step, codes, (long long)cout * K, offset, wscale,
                      status);
   return check_hip(hipGetLastError(), "pack_weights_ex_kernel launch");
 }
 
-extern "C" int smpq_pack_weights_s2d(const float* w, int cout, int cin, int wlimbs, int8_t* codes, float* wscale,
-                                     int32_t* status, smpq_stream_t stream) {
+extern "C" int smpq_pack_weights_s2d_ex(const float* w, int cout, int cin, const float* step, int wlimbs,
+                                        int8_t* codes, float* wscale, int32_t* status, smpq_stream_t stream) {
   if (!w || !codes || !wscale || !status || cout <= 0 || cin <= 0 || cin > 4)
     return fail(SMPQ_E_INVALID, "smpq_pack_weights_s2d: bad arguments (cin must be 1..4)");
   if (wlimbs < 2 || wlimbs > 3) return fail(SMPQ_E_INVALID, "smpq_pack_weights_s2d: wlimbs must be 2 or 3");
   constexpr int K = 256;  // 4 x 4 taps x 16 space-to-depth channels
   hipLaunchKernelGGL(pack_weights_ex_kernel, dim3(cout), dim3(kQThreads), 0, (hipStream_t)stream, w, cin, 7, 7,
-                     16, K, wlimbs, 1, (const float*)nullptr, codes, (long long)cout * K, (int32_t*)nullptr,
-                     wscale, status);
+                     16, K, wlimbs, 1, step, codes, (long long)cout * K, (int32_t*)nullptr, wscale, status);
   return check_hip(hipGetLastError(), "pack_weights_ex_kernel launch");
+}
+
+extern "C" int smpq_pack_weights_s2d(const float* w, int cout, int cin, int wlimbs, int8_t* codes, float* wscale,
+                                     int32_t* status, smpq_stream_t stream) {
+  return smpq_pack_weights_s2d_ex(w, cout, cin, nullptr, wlimbs, codes, wscale, status, stream);
 }

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must be imported before the library; see module doc
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsmpq.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lib = None
 _lock = threading.Lock()
@@ -44,7 +44,6 @@ _PROTOS = {
     "smpq_act_absmax": (_i, [_vp, _i, _i64, _vp, _vp]),
     "smpq_act_quantize": (_i, [_vp, _i, _i64, _vp, _i, _vp, _vp]),
     "smpq_pack_weights_ex": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
-    "smpq_image_quantize": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
     "smpq_maxpool_quantize": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp]),
     "smpq_conv2d_fwd_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp,
                                 _vp, _i, _i, _vp, _vp, _i, _vp]),
@@ -58,6 +57,7 @@ _PROTOS = {
     "smpq_maxpool_limbs": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "smpq_image_quantize_s2d": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
     "smpq_pack_weights_s2d": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "smpq_pack_weights_s2d_ex": (_i, [_vp, _i, _i, _vp, _i, _vp, _vp, _vp, _vp]),
     "smpq_stem_conv_s2d_q": (_i, [_vp, _vp, _i, _i, _i, _vp, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp,
                                   ctypes.c_float, _vp, _i, _vp]),
     "smpq_stem_pool_supported": (_i, [_i] * 6),

@@ -21,15 +21,21 @@ def shard_range(global_batch, rank, world):
     return start, start + base + (1 if rank < rem else 0)
 
 
-def gather_logits(local, world, out=None):
-    """All-gather equal-size per-rank logits [b, C] into [world*b, C] in rank order."""
+def gather_logits(local, world, out=None, group=None):
+    """All-gather equal-size per-rank logits [b, C] into [world*b, C] in rank order (RCCL over
+    xGMI; a gloo group — the multi-process tests that share one GPU — gathers through the host)."""
     if world == 1:
         return local
     local = local.contiguous()
     if out is None:
         out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
                           device=local.device)
-    dist.all_gather_into_tensor(out, local)
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(h, local.cpu(), group=group)
+        out.copy_(h)
+        return out
+    dist.all_gather_into_tensor(out, local, group=group)
     return out
 
 
@@ -60,7 +66,12 @@ def all_reduce_stats(stats, world):
     batches] or smpq_kl_rows' [kl_sum, rows], float64) over ranks: the only collective the
     sharded evaluation needs (SURVEY.md 8(f) rank 1 — a few scalars instead of the logits)."""
     if world > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+        if stats.is_cuda and dist.get_backend() == "gloo":
+            h = stats.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM)
+            stats.copy_(h)
+        else:
+            dist.all_reduce(stats, op=dist.ReduceOp.SUM)
     return stats
 
 

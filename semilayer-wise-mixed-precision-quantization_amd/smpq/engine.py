@@ -292,27 +292,25 @@ def block_forward(blk, x, ctx=None, last=False):
 
 
 def stem_s2d_plan(conv, bn):
-    """(codes, col_scale, col_shift) of the stem in space-to-depth form (ops.stem_conv_s2d), or
+    """(codes, col_scale, col_shift, kind) of the stem in space-to-depth form (ops.stem_conv_s2d), or
     None when conv1 is not the 7x7/2/3 stem on <= 4 channels. Its fp32 weights become per-channel
-    fixed point with max(2, L) limbs, exactly as conv_plan's 'fixed' kind (same codes)."""
-    if not (isinstance(conv, QConv2d) and conv.weight.is_cuda and conv.in_channels <= 4
-            and conv.kernel_size == (7, 7) and conv.stride == (2, 2) and conv.padding == (3, 3)
-            and conv.dilation == (1, 1) and conv.groups == 1 and conv.out_channels % 16 == 0
-            and not (conv._bits_host > 0).any()):
+    fixed point with max(2, L) limbs (quantized channels, if any: exact codes), as in
+    QConv2d.packed_s2d."""
+    if not (isinstance(conv, QConv2d) and conv.s2d_stem()):
         return None
     key = (conv._pack_key(), _bn_key(bn), None if conv.bias is None else (conv.bias.data_ptr(), conv.bias._version))
     cache = getattr(conv, "_s2d_cache", None)
     if cache is not None and cache[0] == key:
         return cache[1]
     with torch.no_grad():
-        codes, wscale = ops.pack_weights_s2d(conv.weight.detach().float(), max(2, ops.get_act_limbs()))
+        codes, wscale, kind = conv.packed_s2d()
         if bn is not None:
             a, b = _bn_fold(bn)
         else:
             a, b = torch.ones_like(wscale), torch.zeros_like(wscale)
         if conv.bias is not None:
             b = b + conv.bias.float() * a
-        plan = (codes, (wscale * a).contiguous(), b.contiguous())
+        plan = (codes, (wscale * a).contiguous(), b.contiguous(), kind)
     conv._s2d_cache = (key, plan)
     return plan
 
@@ -320,26 +318,30 @@ def stem_s2d_plan(conv, bn):
 def stem_forward(model, x, ctx=None):
     """conv1 7x7/2 + bn1 + relu + maxpool 3x3/2 (resnet.py:206-209) -> Act of the pooled output.
     Static-range mode: the stem writes its calibrated-range limb planes and the max pool works on
-    the codes (exact: the quantizer is monotone); no fp32 tensor is written."""
+    the codes (exact: the quantizer is monotone); no fp32 tensor is written. A stem the kernel does
+    not cover (not 7x7/2/3, or other input channels than the conv's) runs on torch, counted in
+    stats['fp32_conv'] like every such conv."""
     x = x.float().contiguous()
     n = x.shape[0]
     pool_ok = isinstance(model.maxpool, torch.nn.MaxPool2d) and model.maxpool.kernel_size in (3, (3, 3)) \
         and model.maxpool.stride in (2, (2, 2)) and model.maxpool.padding in (1, (1, 1))
-    s2d = stem_s2d_plan(model.conv1, model.bn1) if (pool_ok and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0) \
-        else None
+    s2d = stem_s2d_plan(model.conv1, model.bn1) if (pool_ok and x.shape[1] == model.conv1.in_channels
+                                                    and x.shape[2] >= 2 and x.shape[3] >= 2) else None
     if s2d is not None:
-        # space-to-depth stem: 16-channel pixels, K steps of whole tap rows (LDS-DMA kernel)
-        codes, col_scale, col_shift = s2d
+        # space-to-depth stem: 16-channel pixels, K steps of whole tap rows (an odd h or w gets a
+        # zero row / column: the conv's own padding)
+        codes, col_scale, col_shift, kind = s2d
         amax_in = ops.act_absmax(x)
         xq = ops.image_quantize_s2d(x, amax_in)
         stats["hip_conv"] += 1
-        stats["fixed_conv"] += 1
-        model.conv1.last_path = "hip-fixed-s2d"
+        if kind == "fixed":
+            stats["fixed_conv"] += 1
+        model.conv1.last_path = "hip-%s-s2d" % kind
         conv = model.conv1
         if ctx is not None and ctx.ranges is not None and id(conv) in ctx.ranges and conv.out_channels % 16 == 0:
             rng = ctx.ranges[id(conv)]
             if FUSED_STEM[0] and conv.out_channels == 64 and ops.stem_pool_supported(xq, codes, x.shape[2], x.shape[3]):
-                model.conv1.last_path = "hip-fixed-s2d-pool"
+                model.conv1.last_path = "hip-%s-s2d-pool" % kind
                 yq = ops.stem_pool_s2d(xq, amax_in, codes, x.shape[2], x.shape[3], col_scale, col_shift,
                                        emit_range=rng, overflow=ctx.overflow)
                 return Act(q=yq, amax=ctx.range_tensor(conv), rng=rng)
@@ -355,13 +357,9 @@ def stem_forward(model, x, ctx=None):
             ctx.record[id(conv)] = m if prev is None else torch.maximum(prev, m)
         q, f = ops.maxpool_quantize(y, yam, want_f32=True)
         return Act(f32=f, q=q, amax=yam)
-    plan = conv_plan(model.conv1, model.bn1)
-    if plan is not None and x.shape[1] <= 4 and pool_ok:
-        amax_in = ops.act_absmax(x)
-        xq = ops.image_quantize(x, amax_in)
-        stem = run_conv(model.conv1, model.bn1, Act(q=xq, amax=amax_in), relu=True)
-        q, f = ops.maxpool_quantize(stem.f32, stem.amax, want_f32=True)
-        return Act(f32=f, q=q, amax=stem.amax)
+    # a stem the kernel does not cover: the reference's fp32 arithmetic (MIOpen), then quantized
+    stats["fp32_conv"] += 1
+    model.conv1.last_path = "fp32"
     h = model.maxpool(model.relu(model.bn1(model.conv1(x.contiguous(memory_format=torch.channels_last)))))
     h = _to_nhwc(h)
     amax = ops.act_absmax(h)
@@ -582,18 +580,39 @@ def _static_eager(model, x, cal):
     return y, ctx.overflow
 
 
+def _graph_base(cal):
+    """What every captured graph of a model depends on besides its input's shape and address:
+    the calibration (ranges, signature) and the forward's structure knobs."""
+    return (cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0], CONCURRENT_DS[0], STREAMS[0],
+            ops.KMAJOR[0])
+
+
 def _graph_key(model, x, cal):
-    return (tuple(x.shape), x.dtype, x.device, cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0],
-            CONCURRENT_DS[0], STREAMS[0], ops.KMAJOR[0])
+    return (tuple(x.shape), x.dtype, x.device) + _graph_base(cal)
+
+
+def _addr_key(x):
+    """Per-address graph key of an input: its shape, dtype, device and address. A graph captured on
+    an input reads it as a contiguous NCHW tensor, so only contiguous inputs ever match one."""
+    return (tuple(x.shape), x.dtype, x.device, x.data_ptr()) if x.is_contiguous() else None
+
+
+def _graphs(model, cal):
+    """The model's per-address graphs for calibration ``cal`` (dropped when it changes; graphs of
+    other input shapes are kept, so a short last batch does not evict the full-batch graphs)."""
+    per = getattr(model, "_smpq_graphs", None)
+    base = _graph_base(cal)
+    if per is None or per.get("base") != base:
+        per = model._smpq_graphs = {"base": base}
+    return per
 
 
 def _graph_ready(model, x, cal):
-    key = _graph_key(model, x, cal)
-    per_ptr = getattr(model, "_smpq_graphs", None)
-    if per_ptr is not None and (key, x.data_ptr()) in per_ptr:
+    ak = _addr_key(x)
+    if ak is not None and ak in _graphs(model, cal):
         return True
     entry = getattr(model, "_smpq_graph", None)
-    return entry is not None and entry[0] == key
+    return entry is not None and entry[0] == _graph_key(model, x, cal)
 
 
 # HIP graphs captured on an input tensor's own memory (no copy of the input into the graph's static
@@ -605,8 +624,13 @@ GRAPHS_PER_MODEL = [int(_os.environ.get("SMPQ_GRAPHS", "4"))]
 def _capture(model, x_in, cal):
     g = torch.cuda.CUDAGraph()
     ctx = Ctx(x_in.shape[0], x_in.device, ranges=cal[0], cache=cal[2])
+    # one memory pool for all of the model's graphs: they are replayed one at a time on one stream
+    # and each replay's outputs are copied out before the next, so they may share blocks
+    pool = getattr(model, "_smpq_pool", None)
+    if pool is None or pool[0] != x_in.device:
+        pool = model._smpq_pool = (x_in.device, torch.cuda.graph_pool_handle())
     torch.cuda.synchronize()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, pool=pool[1]):
         ctx.overflow = torch.zeros(2, dtype=torch.int32, device=x_in.device)
         y_static = _forward(model, x_in, ctx)
         cal[3].check(ctx.overflow[1:])
@@ -616,25 +640,25 @@ def _capture(model, x_in, cal):
 
 def _graph_forward(model, x, cal):
     """Static forward through a captured HIP graph; returns (logits, overflow flag tensor). The
-    graph reads the input where it lies when its address has a graph of its own (captured on first
-    sight, up to GRAPHS_PER_MODEL addresses, dropped with the calibration); otherwise the input is
-    copied into the fallback graph's static buffer."""
+    graph reads the input where it lies when its (contiguous) input's address has a graph of its
+    own (captured on first sight, up to GRAPHS_PER_MODEL addresses per input shape, dropped with
+    the calibration); otherwise the input is copied into the fallback graph's static buffer."""
     key = _graph_key(model, x, cal)
-    per_ptr = getattr(model, "_smpq_graphs", None)
-    if per_ptr is None or per_ptr.get("key") != key:
-        per_ptr = model._smpq_graphs = {"key": key}
-    hit = per_ptr.get((key, x.data_ptr()))
+    per_ptr = _graphs(model, cal)
+    ak = _addr_key(x)
+    hit = per_ptr.get(ak) if ak is not None else None
     if hit is not None:
         g, ctx, y_static = hit
         g.replay()
         stats["graph_replays"] += 1
         return y_static.clone(), ctx.overflow
-    if len(per_ptr) - 1 < GRAPHS_PER_MODEL[0] and x.is_contiguous():
+    same_shape = sum(1 for k in per_ptr if k != "base" and k[:3] == ak[:3]) if ak is not None else 0
+    if ak is not None and same_shape < GRAPHS_PER_MODEL[0]:
         y, ovf = _static_eager(model, x, cal)  # warm every cache outside the capture
         if any(ovf.tolist()):
             return y, ovf
         g, ctx, y_static = _capture(model, x, cal)
-        per_ptr[(key, x.data_ptr())] = (g, ctx, y_static)
+        per_ptr[ak] = (g, ctx, y_static)
         return y, ovf
     entry = getattr(model, "_smpq_graph", None)
     if entry is None or entry[0] != key:
@@ -642,7 +666,7 @@ def _graph_forward(model, x, cal):
         y, ovf = _static_eager(model, x, cal)
         if any(ovf.tolist()):
             return y, ovf
-        static_x = x.clone()
+        static_x = x.contiguous().clone()
         g, ctx, y_static = _capture(model, static_x, cal)
         model._smpq_graph = (key, g, static_x, ctx, y_static)
         return y, ovf
@@ -684,11 +708,13 @@ def forward_fused(model, x):
     cal = getattr(model, "_smpq_ranges", None)
     fresh = model.__dict__.pop("_smpq_recal", False)
     if _DP[0] is not None:
-        # collective decision: every rank calibrates, or none does
-        need = torch.tensor([0 if (cal is not None and cal[1] == _signature(model) and not fresh) else 1],
-                            dtype=torch.int32, device=x.device)
-        if int(_dp_max_(need).item()):
-            return calibrate(model, x, fresh=fresh)
+        # collective decision: every rank calibrates, or none does; and if any rank starts a new
+        # evaluation, all of them calibrate afresh (the same widening rule on every rank)
+        flags = torch.tensor([0 if (cal is not None and cal[1] == _signature(model)) else 1, int(fresh)],
+                             dtype=torch.int32, device=x.device)
+        need, fresh_any = _dp_max_(flags).tolist()
+        if need or fresh_any:
+            return calibrate(model, x, fresh=bool(fresh_any))
         y, ovf = _graph_forward(model, x, cal) if USE_GRAPH[0] else _static_eager(model, x, cal)
         _dp_max_(ovf)
     else:

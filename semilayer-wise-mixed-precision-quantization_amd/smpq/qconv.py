@@ -15,8 +15,10 @@ the integer path.
 Channels that were never quantized (bit 32 in the reference's bookkeeping: the stem, the
 downsample convs, mid-search semilayers) have no integer code; they run on the same HIP kernel
 with their fp32 weights in per-channel fixed point with as many int8 limbs as the activations
-(16 or 24 bits), counted in ``smpq.stats["fixed_conv"]``. Only geometries the kernel does not cover (groups, dilation,
-cin not in {<=4, 64k}) fall back to ``F.conv2d`` (counted in ``stats["fp32_conv"]``).
+(16 or 24 bits), counted in ``smpq.stats["fixed_conv"]``. The 7x7/2/3 stem on <= 4 channels runs
+as a 4x4 conv over space-to-depth pixels on the same kernel. Only geometries the kernel does not
+cover (groups, dilation, other convs with cin % 64 != 0 or cout % 16 != 0) fall back to
+``F.conv2d`` on the GPU (counted in ``stats["fp32_conv"]``).
 """
 import weakref
 
@@ -119,7 +121,7 @@ class QConv2d(nn.Conv2d):
         return (self.weight.is_cuda and self.groups == 1 and self.dilation == (1, 1)
                 and self.padding_mode == "zeros" and self.stride[0] == self.stride[1]
                 and self.padding[0] == self.padding[1]
-                and (self.in_channels <= 4 or self.in_channels % 64 == 0))
+                and self.in_channels % 64 == 0 and self.out_channels % 16 == 0)
 
     def packed(self):
         """Weight operand of the HIP conv: (codes int8 [LW, cout, K], LW, offset | None,
@@ -154,17 +156,50 @@ class QConv2d(nn.Conv2d):
         self._pack = (key, res)
         return res
 
-    def _s2d_stem(self, x):
-        """The 7x7/2/3 stem on <= 4 channels with every channel unquantized and even h, w."""
-        return (self.in_channels <= 4 and self.kernel_size == (7, 7) and self.stride == (2, 2)
-                and self.padding == (3, 3) and self.groups == 1 and self.dilation == (1, 1)
-                and self.out_channels % 16 == 0 and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0
-                and not (self._bits_host > 0).any())
+    def s2d_stem(self):
+        """Is this the 7x7/2/3 stem on <= 4 channels (resnet.py:143) that runs as a 4x4 conv over
+        space-to-depth pixels?"""
+        return (self.weight.is_cuda and self.in_channels <= 4 and self.kernel_size == (7, 7)
+                and self.stride == (2, 2) and self.padding == (3, 3) and self.groups == 1
+                and self.dilation == (1, 1) and self.padding_mode == "zeros" and self.out_channels % 16 == 0)
+
+    def packed_s2d(self):
+        """Weight operand of the space-to-depth stem: (codes int8 [LW, cout, 256], wscale fp32
+        [cout], kind); quantized channels as exact codes, the others in per-channel fixed point
+        with LW = max(2, L) limbs (kind 'fixed' when any channel is, else 'exact16')."""
+        key = self._pack_key()
+        cached = getattr(self, "_s2d_pack", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        with torch.no_grad():
+            quantized = (self._bits_host > 0).any()
+            codes, wscale = ops.pack_weights_s2d(self.weight.detach().float(), max(2, ops.get_act_limbs()),
+                                                 step=self.qstep if quantized else None)
+        res = (codes, wscale, "exact16" if self.fully_quantized() else "fixed")
+        stats["repack"] += 1
+        self._s2d_pack = (key, res)
+        return res
 
     # ---- forward (module path; the fused ResNet path is smpq.engine) ------------------------
     def forward(self, x):
         if not x.is_cuda:
             raise RuntimeError("smpq QConv2d is MI355X-native: move the model and input to the GPU")
+        if self.s2d_stem() and x.shape[1] == self.in_channels and x.shape[2] >= 2 and x.shape[3] >= 2:
+            # the reference's 7x7/2/3 stem (resnet.py:143): space-to-depth planes on the conv kernel,
+            # the same codes and results as the engine's stem (engine.stem_s2d_plan)
+            codes, s2d_scale, kind = self.packed_s2d()
+            stats["hip_conv"] += 1
+            if kind == "fixed":
+                stats["fixed_conv"] += 1
+            self.last_path = "hip-%s-s2d" % kind
+            xc = x.float().contiguous()
+            amax = ops.act_absmax(xc)
+            xq = ops.image_quantize_s2d(xc, amax)
+            shift = self.bias.detach().float().contiguous() if self.bias is not None else \
+                torch.zeros(self.out_channels, dtype=torch.float32, device=x.device)
+            y = ops.tuned_stem_conv_s2d(xq, amax, codes, x.shape[2], x.shape[3], s2d_scale.contiguous(), shift,
+                                        relu=False)
+            return y.permute(0, 3, 1, 2)
         pk = self.packed()
         if pk is None:
             stats["fp32_conv"] += 1
@@ -176,31 +211,9 @@ class QConv2d(nn.Conv2d):
             stats["fixed_conv"] += 1
         self.last_path = "hip-" + kind
         x = x.float()
-        if self._s2d_stem(x):
-            # the reference's 7x7/2/3 stem (resnet.py:143): space-to-depth planes on the LDS-DMA
-            # kernel, the same codes and results as the engine's stem (engine.stem_s2d_plan)
-            xc = x.contiguous()
-            amax = ops.act_absmax(xc)
-            xq = ops.image_quantize_s2d(xc, amax)
-            key = self._pack_key()
-            cached = getattr(self, "_s2d_pack", None)
-            if cached is None or cached[0] != key:
-                cached = self._s2d_pack = (key,) + ops.pack_weights_s2d(self.weight.detach().float(),
-                                                                       max(2, ops.get_act_limbs()))
-            codes, s2d_scale = cached[1], cached[2]
-            shift = self.bias.detach().float().contiguous() if self.bias is not None else \
-                torch.zeros(self.out_channels, dtype=torch.float32, device=x.device)
-            y = ops.tuned_stem_conv_s2d(xq, amax, codes, x.shape[2], x.shape[3], s2d_scale.contiguous(), shift,
-                                        relu=False)
-            return y.permute(0, 3, 1, 2)
-        if self.in_channels <= 4:
-            xc = x.contiguous()
-            amax = ops.act_absmax(xc)
-            xq = ops.image_quantize(xc, amax)
-        else:
-            xh = x.permute(0, 2, 3, 1).contiguous()
-            amax = ops.act_absmax(xh)
-            xq = ops.act_quantize(xh, amax)
+        xh = x.permute(0, 2, 3, 1).contiguous()
+        amax = ops.act_absmax(xh)
+        xq = ops.act_quantize(xh, amax)
         shift = self.bias.detach().float().contiguous() if self.bias is not None else \
             torch.zeros(self.out_channels, dtype=torch.float32, device=x.device)
         y = ops.tuned_conv2d_q(xq, amax, codes, offset, self.kernel_size[0], self.kernel_size[1],

@@ -285,6 +285,7 @@ def make_model_goldens(functions, resnet, assigns, only=None):
         # name, arch, assignment, batch, recalibrate
         ("r18_fp32", "resnet18", None, 2, False),
         ("r18_u8", "resnet18", "r18_u8", 2, False),
+        ("r18_u8_b1", "resnet18", "r18_u8", 1, False),  # BASELINE configs[0]'s shape (resnet18_main.py, B=1)
         ("r50_mixed", "resnet50", "r50_mixed", 2, False),
         ("r34_4bit", "resnet34", "r34_4bit", 2, False),
         ("r18_u8_cal", "resnet18", "r18_u8", 16, True),

@@ -1,4 +1,5 @@
-"""World-size-2 gloo tests of the data-parallel sharding + logits all-gather (CPU)."""
+"""World-size-2 gloo tests of the data-parallel sharding + logits all-gather (CPU). The real model
+path with two live processes on the GPU is tests/test_gpu_mp.py."""
 import os
 import socket
 
@@ -17,10 +18,18 @@ def _free_port():
 
 
 def _model(x):
-    # a per-image deterministic function standing in for the network
-    g = torch.Generator().manual_seed(0)
-    w = torch.randn(x[0].numel(), 10, generator=g)
-    return x.flatten(1) @ w
+    """The reference's CPU forward of a seeded ResNet-18 (oracle.torch_ref: the torch operators of
+    resnet.py:204-220), in float64 so that every image's logits are the same bits in any batch."""
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (repo, os.path.join(repo, "semilayer-wise-mixed-precision-quantization_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import resnet
+    from oracle import torch_ref
+    torch.manual_seed(0)
+    sd = {k: v.double() for k, v in resnet.resnet18().state_dict().items() if v.is_floating_point()}
+    return torch_ref.resnet_forward("resnet18", sd, x.double())
 
 
 def _worker(rank, world, port, q):
@@ -32,7 +41,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from smpq import dp
-        x = torch.randn(8, 3, 4, 4, generator=torch.Generator().manual_seed(1))
+        x = torch.randn(8, 3, 64, 64, generator=torch.Generator().manual_seed(1))
         y = dp.sharded_forward(_model, x, rank, world)
         q.put((rank, y))
     finally:
@@ -51,8 +60,9 @@ def test_sharded_forward_equals_single_process(world):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    x = torch.randn(8, 3, 4, 4, generator=torch.Generator().manual_seed(1))
+    x = torch.randn(8, 3, 64, 64, generator=torch.Generator().manual_seed(1))
     ref = _model(x)
+    assert ref.shape == (8, 1000)
     for r in range(world):
         assert torch.equal(res[r], ref)
 

@@ -168,7 +168,7 @@ R50_SHAPES = [(64, 64, 1, 1, 56), (64, 64, 3, 1, 56), (64, 256, 1, 1, 56), (256,
               (128, 128, 3, 1, 28), (512, 256, 1, 1, 28), (256, 256, 3, 2, 28), (256, 1024, 1, 1, 14),
               (1024, 256, 1, 1, 14), (256, 256, 3, 1, 14), (1024, 512, 1, 1, 14), (512, 512, 3, 2, 14),
               (512, 2048, 1, 1, 7), (2048, 512, 1, 1, 7), (512, 512, 3, 1, 7)]
-EDGE_SHAPES = [(64, 80, 3, 2, 9), (128, 48, 1, 2, 15), (192, 100, 3, 1, 5), (64, 16, 3, 1, 1)]
+EDGE_SHAPES = [(64, 80, 3, 2, 9), (128, 48, 1, 2, 15), (192, 112, 3, 1, 5), (64, 16, 3, 1, 1)]
 
 
 def run_conv_case(gpu, cin, cout, k, stride, hin, limbs, seed, signed=False, residual=False, relu=False, batch=2):
@@ -249,7 +249,7 @@ def test_all_tile_configs_bitwise_identical(gpu, shape, limbs):
     shift = torch.linspace(-1, 1, cout, device=gpu)
     outs = []
     for c in ops.tile_configs():
-        if not ops._tile_fits(c, limbs, 1, False, cout, cin, k):
+        if not ops._tile_fits(c, limbs, 1, cout, cin, k):
             continue
         ya = torch.zeros(3, device=gpu)
         y = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, residual=res, relu=True,
@@ -269,7 +269,7 @@ def test_all_tile_configs_bitwise_identical(gpu, shape, limbs):
                          ids=lambda s: "c%d_o%d_k%d_s%d_h%d" % s)
 def test_static_outputs_identical_across_tiles(gpu, shape, limbs, range_frac):
     """Static-range epilogue: limb-plane output (next conv's input), limb-plane residual, overflow
-    flag and fp32 output agree bitwise across every tile config of both kernel families, and the
+    flag and fp32 output agree bitwise across every tile config, and the
     emitted digits are clamp(rne(y * QMAX / range))."""
     from smpq import ops
     cin, cout, k, s, h = shape
@@ -287,7 +287,7 @@ def test_static_outputs_identical_across_tiles(gpu, shape, limbs, range_frac):
     rng = float(ref.abs().max()) * range_frac
     outs = []
     for c in ops.tile_configs():
-        if not ops._tile_fits(c, limbs, 1, False, cout, cin, k):
+        if not ops._tile_fits(c, limbs, 1, cout, cin, k):
             continue
         ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
         y, yq = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, relu=True, tile_cfg=c,
@@ -336,7 +336,7 @@ def test_lean_static_epilogue(gpu, shape, limbs, range_frac, relu):
     rng = float(ref.abs().max()) * range_frac
     outs = []
     for c in ops.tile_configs():
-        if not ops._tile_fits(c, limbs, 1, False, cout, cin, k) or ops.tile_kind(c) not in (ops.TILE_LDS_DMA,
+        if not ops._tile_fits(c, limbs, 1, cout, cin, k) or ops.tile_kind(c) not in (ops.TILE_LDS_DMA,
                                                                                             ops.TILE_LDS_DMA_K128):
             continue
         ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
@@ -363,6 +363,19 @@ def test_lean_static_epilogue(gpu, shape, limbs, range_frac, relu):
     if relu:
         assert lean.min() >= 0
     assert int(ovf0.item()) == int(ovf_full.item()) == (1 if range_frac < 1 else 0)
+
+
+def test_conv_rejects_unsupported_geometry(gpu):
+    """cout % 16 != 0 (the reference's ResNets never have it) is refused with a clean error by the
+    C-ABI, before any launch; QConv2d sends such a conv to torch (stats['fp32_conv'])."""
+    from smpq import _lib, ops
+    from smpq.qconv import QConv2d
+    wd, step, codes, offset = make_layer(gpu, 64, 100, 3, seed=5)
+    x = torch.randn(1, 6, 6, 64, generator=torch.Generator().manual_seed(6)).to(gpu)
+    am = ops.act_absmax(x)
+    with pytest.raises((ValueError, _lib.SmpqError), match="multiple of 16"):
+        ops.conv2d_q(ops.act_quantize(x, am, 3), am, codes, offset, 3, 3, 1, 1, step, torch.zeros(100, device=gpu))
+    assert not QConv2d(64, 100, 3, padding=1).to(gpu).hip_supported()
 
 
 def test_conv_offsets_exercised(gpu):
@@ -398,7 +411,7 @@ def build_model(gpu, arch, assign, cal_case=None):
 @pytest.mark.parametrize("mode", ["static", "dynamic"])
 @pytest.mark.parametrize("limbs", [2, 3])
 @pytest.mark.parametrize("case,arch,assign,batch", [
-    ("r18_u8", "resnet18", "r18_u8", 2), ("r50_mixed", "resnet50", "r50_mixed", 2),
+    ("r18_u8", "resnet18", "r18_u8", 2), ("r18_u8_b1", "resnet18", "r18_u8", 1), ("r50_mixed", "resnet50", "r50_mixed", 2),
     ("r34_4bit", "resnet34", "r34_4bit", 2), ("r18_u8_cal", "resnet18", "r18_u8", 16),
     ("r50_mixed_cal", "resnet50", "r50_mixed", 8)])
 def test_model_logits_vs_reference(gpu, case, arch, assign, batch, limbs, mode):
@@ -625,7 +638,7 @@ def test_conv_weight_limbs_vs_emulation(gpu, limbs, wlimbs):
     outs = []
     kinds = set()
     for c in ops.tile_configs():
-        if ops._tile_fits(c, limbs, wlimbs, False, cout, cin, k):
+        if ops._tile_fits(c, limbs, wlimbs, cout, cin, k):
             outs.append(ops.conv2d_q(xq, am, codes, None, k, k, s, 1, cs, sh, residual=res, relu=True, tile_cfg=c))
             kinds.add(ops.tile_kind(c))
     assert ops.TILE_LDS_DMA in kinds and ops.TILE_LDS_DMA_K128 in kinds
@@ -638,94 +651,136 @@ def test_conv_weight_limbs_vs_emulation(gpu, limbs, wlimbs):
     assert (err <= 2e-6 * bound + 1e-30).all()
 
 
-def test_image_quantize_and_stem_conv(gpu):
-    from smpq import ops
-    g = torch.Generator().manual_seed(8)
-    x = torch.randn(2, 3, 40, 40, generator=g).to(gpu)
-    x[1] *= 3
-    am = ops.act_absmax(x)
-    np.testing.assert_array_equal(am.cpu().numpy(), x.abs().amax(dim=(1, 2, 3)).cpu().numpy())
-    xq = ops.image_quantize(x, am, 2)
-    assert xq.shape == (2, 2, 40, 40, 4)
-    q = xq[0].long() + 256 * xq[1].long()
-    inv = (np.float32(32512.0) / am.cpu().numpy()).astype(np.float32)
-    exp = np.rint((x.permute(0, 2, 3, 1).cpu().numpy() * inv[:, None, None, None]).astype(np.float32))
-    np.testing.assert_array_equal(q[..., :3].cpu().numpy(), exp.astype(np.int64))
-    assert int(q[..., 3].abs().max()) == 0
-    w = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(gpu)
-    codes, _, wscale, _ = ops.pack_weights_ex(w, None, 2)
-    assert codes.shape == (2, 64, 256)
-    cs = (wscale * 1.5).contiguous()
-    sh = torch.full((64,), 0.01, device=gpu)
-    yam = torch.zeros(2, device=gpu)
-    y = ops.conv2d_q(xq, am, codes, None, 7, 7, 2, 3, cs, sh, relu=True, y_absmax=yam)
-    assert y.shape == (2, 20, 20, 64)
-    # emulation on the 4-channel planes; weights in [tap][4] order
-    wq = np.zeros((2, 64, 7, 7, 4), np.int64)
-    cr = codes.cpu().numpy().astype(np.int64)[:, :, :196].reshape(2, 64, 7, 7, 4)
-    wq[:] = cr
-    rscale = (am.cpu().numpy() * np.float32(1.0 / 32512.0)).astype(np.float64)
-    ye, bound = emulate_limbs(xq.cpu().numpy(), wq, 7, 2, 3, rscale, cs.cpu().numpy().astype(np.float64),
-                              sh.cpu().numpy().astype(np.float64), None, True)
-    assert (np.abs(y.cpu().numpy() - ye) <= 2e-6 * bound + 1e-30).all()
-    np.testing.assert_array_equal(yam.cpu().numpy(), np.abs(y.cpu().numpy()).reshape(2, -1).max(1))
-    # vs the fp32 conv of the unquantized tensors (quantization error bound)
-    ref = torch.nn.functional.conv2d(x.double(), w.double(), stride=2, padding=3) * 1.5 + 0.01
-    ref = torch.relu(ref).permute(0, 2, 3, 1).cpu().numpy()
-    assert np.abs(y.cpu().numpy() - ref).max() <= 2e-3 * np.abs(ref).max()
+def s2d_to_image_planes(xs):
+    """Space-to-depth planes [L, n, h2, w2, 16] -> the 4-channel image planes [L, n, 2 h2, 2 w2, 4]
+    they hold (channel (dy*2 + dx)*4 + c = pixel (2i + dy, 2j + dx), channel c)."""
+    L, n, h2, w2, _ = xs.shape
+    return xs.reshape(L, n, h2, w2, 2, 2, 4).transpose(0, 1, 2, 4, 3, 5, 6).reshape(L, n, 2 * h2, 2 * w2, 4)
+
+
+def s2d_codes_to_7x7(codes16):
+    """s2d stem codes [LW, cout, 256] (K order [ty][tx][dy][dx][ci], original tap
+    (2 ty + dy - 1, 2 tx + dx - 1)) -> [LW, cout, 7, 7, 4]; the taps outside 7x7 must be zero."""
+    lw, cout, _ = codes16.shape
+    c = codes16.reshape(lw, cout, 4, 4, 2, 2, 4).astype(np.int64)
+    out = np.zeros((lw, cout, 8, 8, 4), np.int64)  # kernel rows / cols -1 .. 6 at index +1
+    for ty in range(4):
+        for tx in range(4):
+            for dy in range(2):
+                for dx in range(2):
+                    out[:, :, 2 * ty + dy, 2 * tx + dx] = c[:, :, ty, tx, dy, dx]
+    assert not out[:, :, 0].any() and not out[:, :, :, 0].any()
+    return out[:, :, 1:, 1:]
 
 
 @pytest.mark.parametrize("limbs", [2, 3])
-@pytest.mark.parametrize("hw", [(40, 36), (224, 224)])
-def test_stem_s2d_bitwise_matches_4ch_stem(gpu, limbs, hw):
-    """The space-to-depth stem (16-channel pixels, 4x4/1 taps) equals the 4-channel 7x7/2 stem
-    bit for bit: same fixed-point codes, exact integer accumulation, same epilogue."""
+@pytest.mark.parametrize("hw", [(40, 36), (37, 41), (224, 224), (33, 2)])
+def test_image_quantize_s2d_and_stem_conv(gpu, limbs, hw):
+    """The space-to-depth stem (the only stem path since ABI 4): the image quantizer's digits (even
+    and odd sizes: an odd h / w gets a zero row / column), the conv against an exact emulation of
+    the 7x7/2/3 conv on the quantized image, bitwise identical across every tile config (fp32 and
+    limb-plane outputs), and within the activation quantization bound of the fp64 conv."""
     from smpq import _lib, ops
-    g = torch.Generator().manual_seed(21 + limbs)
+    g = torch.Generator().manual_seed(8 + limbs + hw[0])
     h, w = hw
-    wt = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(gpu)
     x = torch.randn(2, 3, h, w, generator=g).to(gpu)
-    x[1] *= 5.0
+    x[1] *= 3
     am = ops.act_absmax(x)
-    lw = max(2, limbs)
-    codes4, _, wscale4, _ = ops.pack_weights_ex(wt, None, lw)
-    codes16, wscale16 = ops.pack_weights_s2d(wt, lw)
-    assert torch.equal(wscale4, wscale16)
-    cs = (wscale4 * torch.linspace(0.5, 2, 64, device=gpu)).contiguous()
-    sh = torch.linspace(-1, 1, 64, device=gpu).contiguous()
-    ya4 = torch.zeros(2, device=gpu)
-    y4 = ops.conv2d_q(ops.image_quantize(x, am, limbs), am, codes4, None, 7, 7, 2, 3, cs, sh, relu=True,
-                      y_absmax=ya4)
     xs = ops.image_quantize_s2d(x, am, limbs)
-    rng = float(y4.abs().max()) * 1.5
-    ovf4 = torch.zeros(1, dtype=torch.int32, device=gpu)
-    _, yq4 = ops.conv2d_q(ops.image_quantize(x, am, limbs), am, codes4, None, 7, 7, 2, 3, cs, sh, relu=True,
-                          emit_range=rng, overflow=ovf4, want_f32=False)
-    tried, yq0 = 0, None
+    assert xs.shape == (limbs, 2, (h + 1) // 2, (w + 1) // 2, 16)
+    img = s2d_to_image_planes(xs.cpu().numpy())
+    q = sum(img[l].astype(np.int64) * 256 ** l for l in range(limbs))
+    qmax = np.float32(LIMB_QMAX[limbs])
+    inv = (qmax / am.cpu().numpy()).astype(np.float32)
+    exp = np.rint((x.permute(0, 2, 3, 1).cpu().numpy() * inv[:, None, None, None]).astype(np.float32))
+    np.testing.assert_array_equal(q[:, :h, :w, :3], exp.astype(np.int64))
+    assert not q[..., 3].any() and not q[:, h:].any() and not q[:, :, w:].any()
+    wt = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(gpu)
+    lw = max(2, limbs)
+    codes16, wscale = ops.pack_weights_s2d(wt, lw)
+    cs = (wscale * torch.linspace(0.5, 2, 64, device=gpu)).contiguous()
+    sh = torch.linspace(-1, 1, 64, device=gpu).contiguous()
+    outs = []
     for c in ops.tile_configs():
-        if ops.tile_kind(c) != ops.TILE_LDS_DMA:
-            continue
         ya = torch.zeros(2, device=gpu)
         try:
             y = ops.stem_conv_s2d(xs, am, codes16, h, w, cs, sh, relu=True, y_absmax=ya, tile_cfg=c)
         except _lib.SmpqError:
-            continue
-        tried += 1
-        assert torch.equal(y, y4), c
-        assert torch.equal(ya, ya4), c
+            continue  # not built for the stem (64 output channels per block only)
+        outs.append((c, y, ya))
+    assert len(outs) >= 3
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    y0 = outs[0][1]
+    assert y0.shape == (2, ho, wo, 64)
+    for c, y, ya in outs[1:]:
+        assert torch.equal(y, y0), c
+        assert torch.equal(ya, outs[0][2]), c
+    rscale = (am.cpu().numpy() * np.float32(1.0 / LIMB_QMAX[limbs])).astype(np.float64)
+    ye, bound = emulate_limbs(img, s2d_codes_to_7x7(codes16.cpu().numpy()), 7, 2, 3, rscale,
+                              cs.cpu().numpy().astype(np.float64), sh.cpu().numpy().astype(np.float64), None, True)
+    assert ye.shape == y0.shape
+    assert (np.abs(y0.cpu().numpy() - ye) <= 2e-6 * bound + 1e-30).all()
+    np.testing.assert_array_equal(outs[0][2].cpu().numpy(), np.abs(y0.cpu().numpy()).reshape(2, -1).max(1))
+    ref = torch.nn.functional.conv2d(x.double(), wt.double(), stride=2, padding=3)
+    ref = torch.relu(ref * (cs / wscale).double()[None, :, None, None] + sh.double()[None, :, None, None])
+    ref = ref.permute(0, 2, 3, 1).cpu().numpy()
+    assert np.abs(y0.cpu().numpy() - ref).max() <= 2e-3 * np.abs(ref).max()
+    # limb-plane output (lean static epilogue): identical across tiles, within a code unit or two of
+    # rne(y * QMAX / range) of the fp32 output
+    rng = float(y0.abs().max()) * 1.5
+    yq0 = None
+    for c, _, _ in outs:
         ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
         _, yq = ops.stem_conv_s2d(xs, am, codes16, h, w, cs, sh, relu=True, tile_cfg=c, emit_range=rng,
                                   overflow=ovf, want_f32=False)
-        # limb planes only: the s2d stem takes the lean static epilogue (1/step folded into the
-        # column scale), identical across its tiles and within a code unit or two of the general
-        # epilogue's (test_lean_static_epilogue)
         yq0 = yq if yq0 is None else yq0
         assert torch.equal(yq, yq0), c
-        assert int(ovf.item()) == 0 == int(ovf4.item())
-    assert tried >= 3
+        assert int(ovf.item()) == 0
     lean = sum(yq0[l].cpu().numpy().astype(np.int64) * 256 ** l for l in range(limbs))
-    full = sum(yq4[l].cpu().numpy().astype(np.int64) * 256 ** l for l in range(limbs))
+    full = np.rint(y0.cpu().numpy() * (qmax / np.float32(rng))).astype(np.int64)
     assert np.abs(lean - full).max() <= (1 if limbs == 2 else 2)
+
+
+@pytest.mark.parametrize("hw", [(224, 224), (225, 223)])
+def test_module_path_stem_is_the_s2d_kernel(gpu, hw):
+    """QConv2d.forward of the stem (the module path the unfused forward and a user's own
+    call take) runs the space-to-depth kernel: bitwise the same as stem_conv_s2d on the packed
+    codes, within the activation-quantization bound of the fp64 conv, odd sizes included."""
+    from smpq import ops
+    net = build_model(gpu, "resnet18", None)
+    conv = net.conv1
+    h, w = hw
+    x = torch.randn(2, 3, h, w, generator=torch.Generator().manual_seed(41)).to(gpu)
+    with torch.no_grad():
+        y = conv(x)
+    assert conv.last_path == "hip-fixed-s2d" and y.shape == (2, 64, (h + 1) // 2, (w + 1) // 2)
+    codes, wscale, _ = conv.packed_s2d()
+    am = ops.act_absmax(x)
+    ref = ops.stem_conv_s2d(ops.image_quantize_s2d(x, am), am, codes, h, w, wscale.contiguous(),
+                            torch.zeros(64, device=gpu), relu=False)
+    assert torch.equal(y, ref.permute(0, 3, 1, 2))
+    f64 = torch.nn.functional.conv2d(x.double(), conv.weight.double(), stride=2, padding=3)
+    bound = 0.5 * (am.double() / LIMB_QMAX[3])[:, None, None, None] * \
+        torch.nn.functional.conv2d(torch.ones_like(x).double(), conv.weight.double().abs(), stride=2, padding=3)
+    assert bool(((y.double() - f64).abs() <= bound * 1.01 + 1e-6 * f64.abs().max()).all())
+
+
+def test_quantized_stem_channels_exact(gpu):
+    """A stem with quantized channels (channel_wise_quantizationperchan on conv1's weight) runs on
+    the s2d kernel with those channels' exact codes (pack_weights_s2d with the recorded steps): its
+    output equals the fp64 conv of the quantized weights on the quantized image."""
+    from smpq import ops
+    g = torch.Generator().manual_seed(19)
+    wt = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(gpu)
+    step = ops.quantize_channels_(wt.reshape(64, -1), [8] * 32 + [0] * 32)
+    for lw in (2, 3):
+        codes16, wscale = ops.pack_weights_s2d(wt, lw, step=step)
+        m = s2d_codes_to_7x7(codes16.cpu().numpy())
+        val = sum(m[l] * 256 ** l for l in range(lw))  # [cout, 7, 7, 4]
+        rec = (val[..., :3].transpose(0, 3, 1, 2) * wscale.cpu().numpy().astype(np.float64)[:, None, None, None])
+        # quantized channels: exact codes (m * 2^-sh * step reproduces the weight bit for bit)
+        np.testing.assert_array_equal(rec[:32].astype(np.float32), wt[:32].cpu().numpy())
+        assert np.abs(rec[32:] - wt[32:].cpu().numpy()).max() <= 0.5 * wscale[32:].max().item() * 1.01
 
 
 @pytest.mark.parametrize("limbs", [1, 2, 3])
@@ -914,14 +969,25 @@ def test_graph_replay_matches_eager(gpu):
             x.copy_(x2)
             g5 = net(x)   # replay of x's graph on new content at the same address
             assert stats["graph_captures"] == c0 + 2 and stats["graph_replays"] == r0 + 3
+            # the same address and shape in another layout (a channels_last view of x's
+            # memory) must not replay x's graph, which reads its input as contiguous NCHW
+            n_, c_, h_, w_ = x.shape
+            xcl = x.as_strided(x.shape, (c_ * h_ * w_, 1, w_ * c_, c_))
+            assert xcl.data_ptr() == x.data_ptr() and not xcl.is_contiguous()
+            g6 = net(xcl)
             engine.GRAPHS_PER_MODEL[0] = 0  # fallback: one graph, inputs copied in
             net._smpq_graphs = None
+            net._smpq_graph = None
             f1, f2, f3 = net(x2), net(x2.clone()), net(x2.clone())
-            assert stats["graph_captures"] == c0 + 3 and stats["graph_replays"] == r0 + 5
+            engine.USE_GRAPH[0] = False
+            e6 = net(xcl.contiguous())
+            engine.USE_GRAPH[0] = True
     finally:
         engine.GRAPHS_PER_MODEL[0] = old
+        engine.USE_GRAPH[0] = True
     assert torch.equal(g1, e1) and torch.equal(g2, e2) and torch.equal(g3, e1) and torch.equal(g4, e2)
     assert torch.equal(g5, e2) and torch.equal(f1, e2) and torch.equal(f2, e2) and torch.equal(f3, e2)
+    assert torch.equal(g6, e6) and not torch.equal(g6, e2)
 
 
 def test_graph_fast_path_never_returns_stale_weights(gpu):
@@ -979,7 +1045,7 @@ def test_tile_configs_deterministic(gpu, shape):
     ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
     y0, q0 = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, tile_cfg=1, emit_range=rng,
                           overflow=ovf, **kw)
-    cfgs = [c for c in ops.tile_configs() if ops._tile_fits(c, limbs, 1, False, cout, cin, k)]
+    cfgs = [c for c in ops.tile_configs() if ops._tile_fits(c, limbs, 1, cout, cin, k)]
     for c in cfgs:
         for rep in range(8):
             y, q = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, tile_cfg=c, emit_range=rng,
@@ -1021,7 +1087,7 @@ def test_kmajor_weights_bitwise(gpu, shape):
     ref = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, wscale, shift, weight_layout="rowmajor", **kw)
     rng = float(ref.abs().max()) * 2.0
     cfgs = [c for c in ops.tile_configs() if ops.tile_kind(c) in (ops.TILE_LDS_DMA, ops.TILE_LDS_DMA_K128)
-            and ops._tile_fits(c, limbs, wl, False, cout, cin, k)]
+            and ops._tile_fits(c, limbs, wl, cout, cin, k)]
     assert cfgs
     for c in cfgs:
         o0 = torch.zeros(1, dtype=torch.int32, device=gpu)

@@ -110,15 +110,16 @@ def seeded_state(arch, assign=None, cal=None):
     return sd
 
 
-@pytest.mark.parametrize("case,arch,assign", [("r18_fp32", "resnet18", None), ("r18_u8", "resnet18", "r18_u8")])
-def test_forward_oracle_vs_reference_logits(case, arch, assign):
+@pytest.mark.parametrize("case,arch,assign,batch", [("r18_fp32", "resnet18", None, 2), ("r18_u8", "resnet18", "r18_u8", 2),
+                                                    ("r18_u8_b1", "resnet18", "r18_u8", 1)])
+def test_forward_oracle_vs_reference_logits(case, arch, assign, batch):
     g = _goldens()
     sd = seeded_state(arch, assign)
     for k in g.files:
         if k.startswith(case + "/qsum/"):
             w = sd[k[len(case + "/qsum/"):]].astype(np.float64)
             np.testing.assert_allclose([w.sum(), np.abs(w).sum()], g[k], rtol=1e-9, atol=1e-9)
-    x = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(1))
+    x = torch.randn(batch, 3, 224, 224, generator=torch.Generator().manual_seed(1))
     np.testing.assert_allclose([x.double().sum().item(), x.double().abs().sum().item()], g[case + "/xsum"], rtol=1e-12)
     out = forward_ref.resnet_forward(arch, sd, x.numpy())
     ref = g[case + "/logits"]

@@ -15,7 +15,7 @@ B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 L = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 rows = list(csv.DictReader(open(path)))
 dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-q = [r for r in rows if "qconv_kernel" in r["Kernel_Name"]]
+q = [r for r in rows if "qconv_" in r["Kernel_Name"]]
 nfwd = len(q) // 48
 shapes = []
 H, inp = 56, 64

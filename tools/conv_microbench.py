@@ -52,7 +52,7 @@ for name, cin, cout, k, s, h, res in SHAPES:
     byt = B * h * h * cin * L + B * ho * ho * cout * L * (2 if res else 1)
     out = []
     for c in ops.tile_configs():
-        if not ops._tile_fits(c, L, 1, False, cout, cin, k) or (CFGS is not None and c not in CFGS):
+        if not ops._tile_fits(c, L, 1, cout, cin, k) or (CFGS is not None and c not in CFGS):
             continue
         kw = dict(emit_range=8.0, overflow=ovf, want_f32=False) if static else {}
         if res:

@@ -5,8 +5,7 @@ set -e
 D=$(cd "$(dirname "$0")/.." && pwd)/semilayer-wise-mixed-precision-quantization_amd/csrc
 T=$(mktemp /tmp/isa_XXXX.hip)
 cat > "$T" <<EOS
-#define SMPQ_KERNEL_ONLY
-#include "$D/conv_glds.hip"
+#include "$D/conv_glds_kernel.h"
 namespace smpq { template __global__ void qconv_glds_kernel<$1>(ConvArgs); }
 EOS
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off --cuda-device-only -S "$T" -o "$2" ${@:3}

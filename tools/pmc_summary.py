@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Average rocprofv3 --pmc counters per qconv_kernel instantiation across one or more
+"""Average rocprofv3 --pmc counters per conv kernel instantiation across one or more
 run_counter_collection.csv files. usage: python tools/pmc_summary.py dir [dir ...]"""
 import csv
 import glob

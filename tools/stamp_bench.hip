@@ -14,7 +14,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "conv_glds.hip"
+#include "conv_glds_kernel.h"
 
 using namespace smpq;
 

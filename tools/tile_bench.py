@@ -66,7 +66,7 @@ for name, cin, cout, k, s, h, res, wl in SHAPES:
     for c in ops.tile_configs():
         if ops.tile_kind(c) not in (ops.TILE_LDS_DMA, ops.TILE_LDS_DMA_K128):
             continue
-        if not ops._tile_fits(c, L, wl, False, cout, cin, k) or (CFGS is not None and c not in CFGS):
+        if not ops._tile_fits(c, L, wl, cout, cin, k) or (CFGS is not None and c not in CFGS):
             continue
         try:
             _, y = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, wscale, shift, tile_cfg=c, **kw)
