@@ -26,12 +26,11 @@ bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int w
   const GldsCfg& c = kGlds[cfg];
   if (cin % 64 != 0 || cout % 16 != 0 || (c.bk == 128 && cin % 128 != 0)) return false;
   if (wlimbs == 3 && limbs != 3) return false;
-  if (c.lo && wlimbs != 1) return false;  // limb-outer: exact int8 weights only
   const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
-  const int accs = (c.lo ? 2 : limbs + wlimbs - 1 - smin) * c.wc * c.wp * 4;
-  if (accs > 128 || (accs == 128 && limbs > 1 && !c.lo)) return false;  // (128 at 2 activation limbs spills)
+  const int accs = (limbs + wlimbs - 1 - smin) * c.wc * c.wp * 4;
+  if (accs > 128 || (accs == 128 && limbs > 1)) return false;  // (128 at 2 activation limbs spills)
   const int bc = 16 * c.wc * c.wavesc, bp = 16 * c.wp * c.wavesp;
-  const int stage = (wlimbs * bc + (c.lo ? 1 : limbs) * bp) * c.bk;
+  const int stage = (wlimbs * bc + limbs * bp) * c.bk;
   const int nsteps = kh * kw * cin / c.bk;
   int lds = (nsteps < c.stages ? nsteps : c.stages) * stage;
   if (c.wc % 4 == 0) {  // worst case: staged output tile + residual tile (static-range epilogue)

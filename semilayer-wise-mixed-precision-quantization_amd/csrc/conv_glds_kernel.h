@@ -72,18 +72,11 @@ __device__ unsigned long long* smpq_stamps;
 // scale / shift and the residual scale, ReLU and the code clamp are one v_med3, and overflow is
 // tracked on the rounded codes — about half the VALU work of the general epilogue per output.
 // The body of one block (block `bid` of `total` blocks of this conv); `lds` = the dynamic LDS.
-// LO (limb-outer, LW == 1): the K loop runs once per activation limb (limb 0's K steps, then limb
-// 1's, ...), a stage holds ONE activation limb, and one int32 accumulator set is folded into an fp32
-// set at each limb boundary: v = fl(acc_0), v = fma(fl(acc_1), 256, v), v = fma(fl(acc_2), 65536, v)
-// — the epilogue's own recombination, in the same order, so the outputs are bitwise those of the
-// limb-inner loop. A third less accumulator state and two thirds less activation LDS per stage
-// (more blocks per CU, 128-B K steps that still fit), for the weight tile staged once per limb.
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
-          bool LEAN = false, bool PIPE = false, bool LO = false>
+          bool LEAN = false, bool PIPE = false>
 __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, int8_t* lds) {
   static_assert(BK == 64 || BK == 128, "BK");
   static_assert(!S2D || BK == 64, "the s2d stem uses 64-B K steps");
-  static_assert(!LO || (LW == 1 && !S2D && !PIPE), "limb-outer: exact int8 weights, no s2d stem, plain K loop");
   constexpr int NW = WAVES_C * WAVES_P;
   constexpr int BC = 16 * WC * WAVES_C;  // channels per block tile
   constexpr int BP = 16 * WP * WAVES_P;  // pixels per block tile
@@ -93,9 +86,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   constexpr int RPP = 1024 / BK;   // rows per 1-KiB DMA piece
   constexpr int CPR = BK / 16;     // 16-B chunks per row
   constexpr int WPIECES = LW * (BC / RPP);
-  constexpr int LS = LO ? 1 : L;  // activation limbs staged per K step
-  constexpr int APIECES = LS * (BP / RPP);
-  constexpr int NA = LO ? 1 : NACC;  // int32 accumulator sets held
+  constexpr int APIECES = L * (BP / RPP);
   constexpr int NPIECE = WPIECES + APIECES;
   constexpr int STAGE = NPIECE * 1024;
   constexpr int WSLOTS = (WPIECES + NW - 1) / NW;
@@ -182,7 +173,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   // bytes between the weight slices of consecutive K steps (row-major: BK along the row; K-major:
   // BK / 64 slices of cout rows)
   const unsigned wstep = __builtin_amdgcn_readfirstlane(a.w_kmajor ? (unsigned)(BK * a.cout) : (unsigned)BK);
-  auto issue = [&](int buf, int kr, int kc, int c0, int ks, int il) {
+  auto issue = [&](int buf, int kr, int kc, int c0, int ks) {
     const unsigned sb = lds0 + buf * STAGE;
 #pragma unroll
     for (int s = 0; s < WSLOTS; ++s) {
@@ -194,7 +185,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     for (int s = 0; s < ASLOTS; ++s) {
       const int p = wave + NW * s;
       if (p < APIECES && !(kAblate & 4)) {
-        const int l = LO ? il : p / (BP / RPP);
+        const int l = p / (BP / RPP);
         unsigned voff;
         if constexpr (S2D) {
           const bool ok = (unsigned)(aih[s] + ks) < (unsigned)a.h;
@@ -209,18 +200,17 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     }
   };
 
-  v4i acc[NA][WC][WP];
-  float facc[LO ? WC : 1][LO ? WP : 1][4];  // LO: the fp32 recombination of the folded limbs
+  v4i acc[NACC][WC][WP];
 #pragma unroll
-  for (int s = 0; s < NA; ++s)
+  for (int s = 0; s < NACC; ++s)
 #pragma unroll
     for (int i = 0; i < WC; ++i)
 #pragma unroll
       for (int j = 0; j < WP; ++j) acc[s][i][j] = v4i{0, 0, 0, 0};
   const bool do_off = (LW == 1) && a.has_offset;
-  int rs[LS][WP];  // per-lane partial pixel sums of activation codes (LW == 1 offset correction)
+  int rs[L][WP];  // per-lane partial pixel sums of activation codes (LW == 1 offset correction)
 #pragma unroll
-  for (int l = 0; l < LS; ++l)
+  for (int l = 0; l < L; ++l)
 #pragma unroll
     for (int j = 0; j < WP; ++j) rs[l][j] = 0;
 
@@ -333,25 +323,21 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   for (int s = 0; s < ASLOTS; ++s) ppw += (wave + NW * s < APIECES) ? 1 : 0;
   if constexpr (kUniform) ppw = PPW;
 
-  int kr = 0, kc = 0, c0 = 0, il = 0;  // K position (and, LO, activation limb) of the next step to issue
+  int kr = 0, kc = 0, c0 = 0;  // K position of the next step to issue
   auto advance = [&]() {
     c0 += BK;
     if (c0 == a.cin) {
       c0 = 0;
       if (++kc == a.kw) {
         kc = 0;
-        if (++kr == a.kh && LO) {
-          kr = 0;
-          ++il;
-        }
+        ++kr;
       }
     }
   };
-  const int ntot = LO ? L * nsteps : nsteps;  // K steps of the whole loop
   int nissued = 0, wbuf = 0, rbuf = 0;
   // fragments of one MFMA K step of a stage
   struct Frags {
-    v4i w[LW][WC], a[LS][WP];
+    v4i w[LW][WC], a[L][WP];
   };
   auto read_frags = [&](Frags& f, const int8_t* sb, int h) {
 #pragma unroll
@@ -360,7 +346,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       for (int i = 0; i < WC; ++i)
         f.w[lw][i] = *reinterpret_cast<const v4i*>(sb + (lw * BC + (wc * WC + i) * 16) * BK + rd[h]);
 #pragma unroll
-    for (int l = 0; l < LS; ++l)
+    for (int l = 0; l < L; ++l)
 #pragma unroll
       for (int j = 0; j < WP; ++j)
         f.a[l][j] = *reinterpret_cast<const v4i*>(sb + WPIECES * 1024 + (l * BP + (wp * WP + j) * 16) * BK + rd[h]);
@@ -368,7 +354,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   auto mma = [&](const Frags& f) {
     if (do_off) {
 #pragma unroll
-      for (int l = 0; l < LS; ++l)
+      for (int l = 0; l < L; ++l)
 #pragma unroll
         for (int j = 0; j < WP; ++j) {
           int s = rs[l][j];
@@ -378,16 +364,6 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
           s = __builtin_amdgcn_sdot4(f.a[l][j].w, 0x01010101, s, false);
           rs[l][j] = s;
         }
-    }
-    if constexpr (LO) {  // one limb per step, one accumulator set
-      if (!(kAblate & 8)) {
-#pragma unroll
-        for (int i = 0; i < WC; ++i)
-#pragma unroll
-          for (int j = 0; j < WP; ++j)
-            acc[0][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.w[0][i], f.a[0][j], acc[0][i][j], 0, 0, 0);
-      }
-      return;
     }
 #pragma unroll
     for (int l = 0; l < L; ++l)
@@ -402,47 +378,9 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
                 __builtin_amdgcn_mfma_i32_16x16x64_i8(f.w[lw][i], f.a[l][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
       }
   };
-  // LO: the end of limb l's K loop: offset correction of its accumulators (8-bit channels off
-  // centre: acc += offset_c * pixel sum of the limb's digits), then fold them into the fp32 set
-  auto fold = [&](int l) {
-    if constexpr (LO) {
-      if (do_off) {
-#pragma unroll
-        for (int j = 0; j < WP; ++j) {
-          int t = rs[0][j];
-          t += __shfl_xor(t, 16, kWave);
-          t += __shfl_xor(t, 32, kWave);
-          rs[0][j] = t;
-        }
-#pragma unroll
-        for (int i = 0; i < WC; ++i) {
-          const int c = chan[i] < a.cout ? chan[i] : 0;
-          const int4 coff = *reinterpret_cast<const int4*>(a.w_off + c);
-          const int cor[4] = {coff.x, coff.y, coff.z, coff.w};
-#pragma unroll
-          for (int j = 0; j < WP; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) acc[0][i][j][r] += __mul24(cor[r], rs[0][j]);
-        }
-#pragma unroll
-        for (int j = 0; j < WP; ++j) rs[0][j] = 0;
-      }
-      const float wl = l == 0 ? 1.f : (l == 1 ? 256.f : 65536.f);
-#pragma unroll
-      for (int i = 0; i < WC; ++i)
-#pragma unroll
-        for (int j = 0; j < WP; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float t = (float)acc[0][i][j][r];
-            facc[i][j][r] = l == 0 ? t : __fmaf_rn(t, wl, facc[i][j][r]);
-            acc[0][i][j][r] = 0;
-          }
-    }
-  };
   auto issue_next = [&]() {
-    if (nissued < ntot) {
-      issue(wbuf, kr, kc, c0, nissued - il * nsteps, il);
+    if (nissued < nsteps) {
+      issue(wbuf, kr, kc, c0, nissued);
       advance();
       ++nissued;
       wbuf = wbuf + 1 == NST ? 0 : wbuf + 1;
@@ -510,10 +448,9 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   } else {
 #pragma unroll
     for (int st = 0; st < NST - 1; ++st)
-      if (st < ntot) issue_next();
+      if (st < nsteps) issue_next();
     SMPQ_STAMP(1);
-    int kl = 0, cur = 0;  // LO: K steps done in the current limb, the current limb
-    for (int ks = 0; ks < ntot; ++ks) {
+    for (int ks = 0; ks < nsteps; ++ks) {
       // this wave's DMA of step ks has landed (the younger steps' may still fly) and its reads of
       // step ks-1 are done; after the barrier every wave's are, so stage ks is readable and the
       // stage of step ks-1 may be refilled
@@ -554,12 +491,6 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
         read_frags(f, sb, h);
         mma(f);
       }
-      if constexpr (LO) {
-        if (++kl == nsteps) {
-          fold(cur++);
-          kl = 0;
-        }
-      }
     }
   }
 
@@ -567,7 +498,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   if constexpr ((kAblate & 16) != 0) {  // diagnostic: no epilogue at all (keep the MFMAs live)
     int keep = 0;
 #pragma unroll
-    for (int q = 0; q < NA; ++q)
+    for (int q = 0; q < NACC; ++q)
 #pragma unroll
       for (int i = 0; i < WC; ++i)
 #pragma unroll
@@ -600,9 +531,9 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
           }
     }
   }
-  if (!LO && do_off) {
+  if (do_off) {
 #pragma unroll
-    for (int l = 0; l < LS; ++l)
+    for (int l = 0; l < L; ++l)
 #pragma unroll
       for (int j = 0; j < WP; ++j) {
         int s = rs[l][j];
@@ -611,7 +542,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
         rs[l][j] = s;
       }
   }
-  if constexpr (SMIN == 0 && !LO) {
+  if constexpr (SMIN == 0) {
     if (do_off) {  // weight offsets (8-bit channels off-centre): acc_l += offset_c * sum of pixel digits_l
 #pragma unroll
       for (int i = 0; i < WC; ++i) {
@@ -652,7 +583,6 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   // limb recombination of the accumulators: v = sum_s fl(acc_s) * 256^(SMIN + s), two channels at
   // a time (v_pk_* fp32 ops round like their scalar forms: the same bits as conv.hip's epilogue)
   auto combine = [&](int i, int j, int h) {
-    if constexpr (LO) return f2{facc[i][j][2 * h], facc[i][j][2 * h + 1]};
     f2 v;
 #pragma unroll
     for (int s = 0; s < NACC; ++s) {
@@ -685,15 +615,11 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       const float shq[4] = {csh.x * inv, csh.y * inv, csh.z * inv, csh.w * inv};
 #pragma unroll
       for (int j = 0; j < WP; ++j) {
-        float m;
-        if constexpr (LO) {
-          m = lean_quad_v<L>(facc[i][j], rscale[j], csq, shq, has_res, rqv[i][j], rsq, relu, lo, wq[i][j]);
-        } else {
-          v4i accq[NACC];
+        v4i accq[NACC];
 #pragma unroll
-          for (int t = 0; t < NACC; ++t) accq[t] = acc[t][i][j];
-          m = lean_quad<L, NACC, SMIN>(accq, rscale[j], csq, shq, has_res, rqv[i][j], rsq, relu, lo, wq[i][j]);
-        }
+        for (int t = 0; t < NACC; ++t) accq[t] = acc[t][i][j];
+        const float m = lean_quad<L, NACC, SMIN>(accq, rscale[j], csq, shq, has_res, rqv[i][j], rsq, relu, lo,
+                                                 wq[i][j]);
         vmax = ooff[i][j] != kOOB ? fmaxf(vmax, m) : vmax;
       }
     }
@@ -873,15 +799,15 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 }
 
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
-          bool LEAN = false, bool PIPE = false, bool LO = false>
+          bool LEAN = false, bool PIPE = false>
 __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // min(NST, ksteps) stages
-  qconv_glds_body<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, LEAN, PIPE, LO>(a, blockIdx.x, gridDim.x, lds);
+  qconv_glds_body<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, LEAN, PIPE>(a, blockIdx.x, gridDim.x, lds);
 }
 
 // ------------------------------------------------------------------------------------------
 struct GldsCfg {
-  int wavesc, wavesp, wc, wp, stages, bk, pipe, lo;  // lo: limb-outer K loop (exact int8 weights only)
+  int wavesc, wavesp, wc, wp, stages, bk, pipe;
 };
 constexpr GldsCfg kGlds[] = {
     {2, 2, 2, 2, 2, 64, 0},  // 0:  64 ch x  64 px, 256 threads
@@ -930,23 +856,12 @@ constexpr GldsCfg kGlds[] = {
     {2, 2, 4, 2, 4, 64, 1},   // 34: as 22
     {1, 4, 4, 1, 4, 64, 1},   // 35: as 24
     {2, 2, 2, 2, 3, 128, 1},  // 36: as 26
-    // limb-outer K loops (LO: one activation limb per stage, one int32 accumulator set folded into
-    // fp32 per limb; exact int8 weights only): less LDS and fewer registers per block
-    {2, 2, 4, 2, 2, 64, 0, 1},   // 37: as 2
-    {2, 2, 4, 2, 2, 128, 0, 1},  // 38: as 18
-    {2, 2, 4, 2, 3, 64, 0, 1},   // 39: as 12
-    {1, 4, 4, 1, 2, 128, 0, 1},  // 40: as 17
-    {2, 2, 4, 1, 2, 128, 0, 1},  // 41: as 19
-    {2, 2, 4, 4, 2, 64, 0, 1},   // 42: 128 ch x 128 px
-    {2, 2, 4, 2, 3, 128, 0, 1},  // 43: as 25
 };
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, bool S2D = false, int NST = 2, int MINW = 2,
-          int BK = 64, bool PIPE = false, bool LO = false>
+          int BK = 64, bool PIPE = false>
 static int launch_one(const ConvArgs& a, hipStream_t stream) {
   constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
-  if constexpr (LO && LW != 1) {
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: limb-outer tile configs take exact int8 weights only");
-  } else if constexpr ((LO ? 2 : L + LW - 1 - SMIN) * WC * WP * 4 > 128) {
+  if constexpr ((L + LW - 1 - SMIN) * WC * WP * 4 > 128) {
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: tile config too large for these limb counts");
   } else {
     constexpr int BC = 16 * WC * WAVES_C, BP = 16 * WP * WAVES_P;
@@ -955,7 +870,7 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
     if (mt * nt > 0x7fffffffL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
     if (BK == 128 && a.cin % 128 != 0)
       return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: 128-wide K steps need cin % 128 == 0");
-    constexpr int STAGE = (LW * BC + (LO ? 1 : L) * BP) * BK;
+    constexpr int STAGE = (LW * BC + L * BP) * BK;
     constexpr int kMaxLds = 160 * 1024;  // LDS per CU on gfx950
     // no more stages than K steps: a single-step conv (1x1, cin 64) needs one
     const int nsteps = a.ksteps / (BK / 64);
@@ -971,8 +886,8 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
     ConvArgs b = a;
     fast_div_init((int)nt, b.ntc_mul, b.ntc_shr);
     const bool lean = L >= 2 && a.yq && !a.y && !a.residual && !a.y_absmax;
-    auto kfull = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, false, PIPE, LO>;
-    auto klean = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, (L >= 2), PIPE, LO>;
+    auto kfull = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, false, PIPE>;
+    auto klean = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, (L >= 2), PIPE>;
     auto set_lds = [](const void* k) {
       const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                kMaxNeed < kMaxLds ? kMaxNeed : kMaxLds);
@@ -1030,13 +945,6 @@ int launch_cfg(int cfg, const ConvArgs& a, hipStream_t s) {
     case 34: return launch_one<L, LW, 2, 2, 4, 2, false, 4, 2, 64, true>(a, s);
     case 35: return launch_one<L, LW, 1, 4, 4, 1, false, 4, 2, 64, true>(a, s);
     case 36: return launch_one<L, LW, 2, 2, 2, 2, false, 3, 2, 128, true>(a, s);
-    case 37: return launch_one<L, LW, 2, 2, 4, 2, false, 2, 4, 64, false, true>(a, s);
-    case 38: return launch_one<L, LW, 2, 2, 4, 2, false, 2, 4, 128, false, true>(a, s);
-    case 39: return launch_one<L, LW, 2, 2, 4, 2, false, 3, 4, 64, false, true>(a, s);
-    case 40: return launch_one<L, LW, 1, 4, 4, 1, false, 2, 4, 128, false, true>(a, s);
-    case 41: return launch_one<L, LW, 2, 2, 4, 1, false, 2, 4, 128, false, true>(a, s);
-    case 42: return launch_one<L, LW, 2, 2, 4, 4, false, 2, 2, 64, false, true>(a, s);
-    case 43: return launch_one<L, LW, 2, 2, 4, 2, false, 3, 2, 128, false, true>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   }
 }

@@ -173,16 +173,6 @@ __device__ __forceinline__ float lean_quad(const v4i* accs, float rscale, const 
   return m;
 }
 
-template <int L>
-__device__ __forceinline__ float lean_quad_v(const float* vs, float rscale, const float* csq, const float* shq,
-                                             bool has_res, const int* rqv, float rsq, bool relu, float lo,
-                                             unsigned* wq) {
-  int q[4];
-  const float m = lean_codes_v<L>(vs, rscale, csq, shq, has_res, rqv, rsq, relu, lo, q);
-  encode4<L>(q, wq);
-  return m;
-}
-
 }  // namespace
 
 template <int N>
