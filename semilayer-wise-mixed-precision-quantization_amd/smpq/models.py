@@ -166,11 +166,20 @@ class ResNet(nn.Module):
         return self._forward_impl(x)
 
     def _apply(self, fn, *args, **kwargs):
-        # .to() / .cuda() / .half() replace buffer tensors: drop the engine's cached references
-        # (signature tensor list, captured graph) so they are rebuilt from the new tensors
-        for k in ("_smpq_graph", "_smpq_graphs", "_smpq_dyn", "_smpq_ranges", "_smpq_fp"):
-            self.__dict__.pop(k, None)
-        return super()._apply(fn, *args, **kwargs)
+        # .to() / .cuda() / .half() that replace parameter or buffer tensors: drop the engine's cached
+        # references (signature tensor list, captured graphs, ranges, fingerprints) so they are
+        # rebuilt from the new tensors. A no-op .to() (the model already there: the reference's
+        # evaluate_acc_loss_softmax calls net.to(device) on every evaluation, functions.py:97) keeps
+        # them: dropping them would recalibrate, repack every weight and recapture every graph.
+        def tensors():
+            return [(id(t), t.data_ptr(), t.dtype, t.device) for t in self.parameters()] + \
+                [(id(t), t.data_ptr(), t.dtype, t.device) for t in self.buffers()]
+        before = tensors()
+        out = super()._apply(fn, *args, **kwargs)
+        if tensors() != before:
+            for k in ("_smpq_graph", "_smpq_graphs", "_smpq_dyn", "_smpq_ranges", "_smpq_fp", "_smpq_pool"):
+                self.__dict__.pop(k, None)
+        return out
 
 
 def _resnet(arch, block, layers, pretrained, progress, **kwargs):

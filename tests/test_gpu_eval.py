@@ -98,3 +98,37 @@ def test_eval_kernels_reject_bad_input(gpu):
         ops.softmax_xent(torch.randn(4, 10, device=gpu).double(), torch.zeros(4, dtype=torch.long), stats)
     with pytest.raises(_lib.SmpqError):
         _lib.check(_lib.load().smpq_softmax_xent(None, None, 4, 10, None, None, None, _lib.stream_ptr()), "x")
+
+
+def test_repeated_evaluations_keep_graphs_and_host_batches_match(gpu):
+    """The reference calls net.to(device) on every evaluation (functions.py:97): a no-op .to() keeps
+    the engine's packed weights, calibration and graphs, so a second evaluation of the same loader
+    captures and repacks nothing (it recalibrates on its first batch, engine.new_evaluation).
+    Host batches (pageable and pinned: DeviceBatches copies them on a side stream) give the same
+    results bit for bit as device batches, and a .to() that really moves the model drops the caches
+    and still gives the same results."""
+    import functions
+    from smpq import stats
+    from test_gpu import build_model
+    net = build_model(gpu, "resnet18", "r18_u8")
+    g = torch.Generator().manual_seed(12)
+    host = [(torch.randn(6, 3, 224, 224, generator=g), torch.randint(0, 1000, (6,), generator=g)) for _ in range(4)]
+    on_dev = [(x.to(gpu), y.to(gpu)) for x, y in host]
+    pinned = [(x.pin_memory(), y.pin_memory()) for x, y in host]
+
+    def same(r, ref):
+        return r[0] == ref[0] and r[1] == ref[1] and all(torch.equal(a, b) for a, b in zip(r[2], ref[2]))
+    ref = functions.evaluate_acc_loss_softmax(net, gpu, on_dev)
+    keys = ("graph_captures", "repack", "calibrations", "graph_replays")
+    s0 = {k: stats[k] for k in keys}
+    again = functions.evaluate_acc_loss_softmax(net, gpu, on_dev)
+    d = {k: stats[k] - s0[k] for k in keys}
+    assert d["graph_captures"] == 0 and d["repack"] == 0 and d["calibrations"] == 1 and d["graph_replays"] == 3, d
+    assert same(again, ref)
+    for loader in (host, pinned):
+        assert same(functions.evaluate_acc_loss_softmax(net, gpu, loader), ref)
+    net.cpu()
+    net.to(gpu)
+    r0 = stats["repack"]
+    assert same(functions.evaluate_acc_loss_softmax(net, gpu, on_dev), ref)
+    assert stats["repack"] > r0
