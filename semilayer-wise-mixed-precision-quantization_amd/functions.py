@@ -13,91 +13,14 @@ reproduce): the dummy sentinel rows appended to the caller's lists, the semilaye
 ``dlists[i][index] <= 0`` indexed by list position (functions.py:171-173), and the sensitivity
 pass quantizing the caller's net for its first semilayer before switching to fresh models.
 """
-import threading
-
 import torch
 
 from smpq import engine, ops
+from smpq.batches import DeviceBatches
 from smpq.models import ResNet
 from smpq.quant import channel_wise_quantizationperchan, quantize_wgt  # noqa: F401
 
 _SENTINEL = [0, 0, 100, 0, 0, 0, 0, 0]
-
-
-class DeviceBatches:
-    """The batches of ``loader`` on ``dev``, with batch i+1's host-to-device copy in flight on a
-    side stream while batch i is being evaluated (the reference copies each batch on the compute
-    stream, functions.py:109-111, so copy and forward alternate). Host batches are copied from
-    pinned memory: a pinned batch (the reference's DataLoader uses pin_memory=True) directly, any
-    other one after a copy into one of two reusable pinned buffers, made on a worker thread while
-    the GPU runs. Device batches pass through untouched."""
-
-    def __init__(self, loader, dev):
-        self.loader, self.dev = loader, dev
-        self.stream = torch.cuda.Stream(device=dev)
-        self._pinned = {}    # (shape, dtype) -> [buffer 0, buffer 1]
-        self._done = [None, None]  # copy-finished event of each pinned slot
-        self._slot = 0
-
-    def _pin(self, t):
-        if t.is_pinned():
-            return t, None
-        key = (tuple(t.shape), t.dtype)
-        bufs = self._pinned.get(key)
-        if bufs is None:
-            bufs = self._pinned[key] = [torch.empty(t.shape, dtype=t.dtype).pin_memory() for _ in range(2)]
-        k = self._slot
-        self._slot ^= 1
-        if self._done[k] is not None:
-            self._done[k].synchronize()  # the slot's previous copy has left the buffer
-        bufs[k].copy_(t)
-        return bufs[k], k
-
-    def _stage(self, x, y):
-        """(x, y) -> device tensors + the event that marks their copy done (None: nothing to wait)."""
-        if x.is_cuda:
-            return x, y, None
-        xp, kx = self._pin(x)
-        yp = y if (not torch.is_tensor(y) or y.is_pinned()) else y.pin_memory()
-        with torch.cuda.stream(self.stream):
-            xd = xp.to(self.dev, non_blocking=True)
-            yd = yp.to(self.dev, non_blocking=True) if torch.is_tensor(yp) else yp
-            ev = torch.cuda.Event()
-            ev.record(self.stream)
-        if kx is not None:
-            self._done[kx] = ev
-        return xd, yd, ev
-
-    def __iter__(self):
-        it = iter(self.loader)
-        nxt = [None]
-
-        def fetch():
-            try:
-                x, y = next(it)
-                with torch.cuda.device(self.dev):
-                    nxt[0] = self._stage(x, y)
-            except StopIteration:
-                nxt[0] = StopIteration
-            except BaseException as e:  # noqa: BLE001 -- re-raised in the consuming thread
-                nxt[0] = e
-        fetch()
-        while nxt[0] is not StopIteration:
-            if isinstance(nxt[0], BaseException):
-                raise nxt[0]
-            xd, yd, ev = nxt[0]
-            worker = threading.Thread(target=fetch)  # stage batch i+1 while batch i runs
-            worker.start()
-            main = torch.cuda.current_stream(self.dev)
-            if ev is not None:
-                main.wait_event(ev)
-                xd.record_stream(main)  # allocated on the copy stream, used on this one
-                if torch.is_tensor(yd):
-                    yd.record_stream(main)
-            try:
-                yield xd, yd
-            finally:
-                worker.join()
 
 
 def _run_eval(net, device, data_loader, want_probs):

@@ -82,18 +82,25 @@ def sharded_eval(net, loader, rank, world, device=None, keep_probs=True):
     Returns (acc, loss, this rank's softmax shards) — the shards stay where they were made and
     feed sharded_kldiv, so no logits or probabilities cross xGMI."""
     from smpq import engine, ops
+    from smpq.batches import DeviceBatches
     from smpq.models import ResNet
     dev = device or torch.device("cuda", torch.cuda.current_device())
     stats = torch.zeros(4, dtype=torch.float64, device=dev)
     probs = []
     if isinstance(net, ResNet):
         engine.new_evaluation(net)  # as functions.evaluate_acc_loss_softmax (history-independent)
-    with torch.no_grad(), lockstep():
+
+    def shards():
         for x, y in loader:
             s, e = shard_range(x.shape[0], rank, world)
             assert (e - s) * world == x.shape[0], "equal shards required (the batch mean of shard means)"
-            out = net(x[s:e].to(dev, non_blocking=True)).float().contiguous()
-            p = ops.softmax_xent(out, y[s:e], stats, want_probs=keep_probs)
+            yield x[s:e], y[s:e]
+    with torch.no_grad(), lockstep():
+        # this rank's shards reach the device as functions.evaluate_acc_loss_softmax's batches do:
+        # the next one's copy on a side stream while this one runs
+        for x, y in DeviceBatches(shards(), dev):
+            out = net(x).float().contiguous()
+            p = ops.softmax_xent(out, y, stats, want_probs=keep_probs)
             if keep_probs:
                 probs.append(p)
     loss_sum, correct, seen, count = all_reduce_stats(stats, world).tolist()
