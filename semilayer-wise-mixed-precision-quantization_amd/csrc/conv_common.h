@@ -85,6 +85,14 @@ int glds_cfg_bk(int cfg);
 bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs);
 int launch_glds(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s);
 int glds_default_cfg(const ConvArgs& a, int limbs, int wlimbs);
+bool glds_is_halo(int cfg);
+
+// halo-patch 3x3 kernel (conv_halo.hip); its tile configs follow the LDS-DMA ones in the C-ABI's
+// numbering (cfg = glds count + halo index)
+int halo_num_cfgs();
+void halo_cfg_info(int cfg, int* bm, int* bn, int* threads);
+bool halo_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs);
+int launch_halo(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s);
 
 // The 4 codes (channels 0..3) held by one dword per limb plane, w[l] = the 4 balanced digits of
 // limb l: q = sum_l d_l 256^l. With u_l = d_l + 128 (byte ^ 0x80) for the low limbs,

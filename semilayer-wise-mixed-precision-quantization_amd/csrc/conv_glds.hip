@@ -17,12 +17,15 @@ SMPQ_GLDS_FAMILY(3, 3)
 
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
-int glds_num_cfgs() { return kNumGlds; }
+int glds_num_cfgs() { return kNumGlds + halo_num_cfgs(); }
 
-int glds_cfg_bk(int cfg) { return kGlds[cfg].bk; }
+bool glds_is_halo(int cfg) { return cfg >= kNumGlds; }
+
+int glds_cfg_bk(int cfg) { return cfg >= kNumGlds ? 64 : kGlds[cfg].bk; }
 
 // Same rules as launch_one / launch_glds (accumulator budget, K-step width, LDS per CU).
 bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs) {
+  if (cfg >= kNumGlds) return halo_supported(cfg - kNumGlds, cin, cout, kh, kw, limbs, wlimbs);
   const GldsCfg& c = kGlds[cfg];
   if (cin % 64 != 0 || cout % 16 != 0 || (c.bk == 128 && cin % 128 != 0)) return false;
   if (wlimbs == 3 && limbs != 3) return false;
@@ -53,12 +56,13 @@ int glds_default_cfg(const ConvArgs& a, int limbs, int wlimbs) {
   if (a.s2d || a.cin % kKStep != 0 || a.cout % 16 != 0 || !glds_planes_ok(a, limbs, wlimbs)) return -1;
   const int first = a.cout <= 64 ? 3 : 2;
   if (glds_supported(first, a.cin, a.cout, a.kh, a.kw, limbs, wlimbs)) return first;
-  for (int c = 0; c < kNumGlds; ++c)
+  for (int c = 0; c < kNumGlds; ++c)  // (never a halo tile: those need the lean epilogue)
     if (glds_supported(c, a.cin, a.cout, a.kh, a.kw, limbs, wlimbs)) return c;
   return -1;
 }
 
 void glds_cfg_info(int cfg, int* bm, int* bn, int* threads) {
+  if (cfg >= kNumGlds) return halo_cfg_info(cfg - kNumGlds, bm, bn, threads);
   const GldsCfg& c = kGlds[cfg];
   *bm = 16 * c.wp * c.wavesp;  // pixels (GEMM rows)
   *bn = 16 * c.wc * c.wavesc;  // channels
@@ -82,6 +86,7 @@ int launch_glds(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s
   if ((!a.s2d && a.cin % kKStep != 0) || a.cout % 16 != 0 || !glds_planes_ok(a, limbs, wlimbs))
     return fail(SMPQ_E_INVALID,
                 "smpq_conv2d_fwd: LDS-DMA tile configs need cin % 64 == 0, cout % 16 == 0 and planes < 2 GiB");
+  if (cfg >= kNumGlds) return launch_halo(cfg - kNumGlds, limbs, wlimbs, a, s);
   if (a.s2d) {
     if (wlimbs == 2 && limbs == 1) return launch_s2d<1, 2>(cfg, a, s);
     if (wlimbs == 2 && limbs == 2) return launch_s2d<2, 2>(cfg, a, s);

@@ -1,0 +1,369 @@
+// Halo-patch 3x3 quantized conv (stride 1, pad 1) for gfx950: the static-range ("lean") forward of
+// the quantized conv2 of BasicBlock / Bottleneck (resnet.py:22-25, 55-68, 97-116), bitwise equal to
+// qconv_glds_kernel (conv_glds_kernel.h) on the same inputs.
+//
+// Why a second kernel for the 3x3 convs: the implicit GEMM stages the activation operand once per
+// TAP — every input pixel crosses L2 -> LDS nine times (3 limbs each), and for the 64- and
+// 128-channel 3x3 convs of the early layers that operand traffic, not the matrix cores, bounds
+// the kernel (tools/batch_scaling.py). Here a block owns TH x TW output pixels of one
+// image and 64 output channels; per 64-channel input chunk it stages
+//   * the (TH + 2) x (TW + 2) input patch of every activation limb ONCE (LDS-DMA, 64 B per pixel),
+//   * the chunk's weights of all nine taps ([tap][64 couts][64 B], from the K-major codes),
+// and runs the nine taps out of LDS: tap (kr, kc) of pixel (r, c) is patch pixel (r + kr, c + kc),
+// so a lane's B-fragment address is a per-lane base plus a compile-time offset per tap and limb.
+// Operand bytes per output pixel and chunk fall from 9 * L * 64 to about (TH+2)(TW+2)/(TH*TW) * L * 64.
+//
+//  * Fragments: pixel fragment f of the block = tile pixels 16 f .. 16 f + 15 in row-major tile
+//    order (2 rows x 8 columns at TW = 8, 4 x 4 at TW = 4); the MFMA is v_mfma_i32_16x16x64_i8 with
+//    A = weights (16 couts x 64 K), B = activations (64 K x 16 pixels) as in qconv_glds_kernel, so
+//    a lane ends with 4 consecutive output channels of one pixel and the epilogue is that kernel's.
+//  * LDS patch image: pixel (pr, pc) of limb l at l * PH * PW * 64 + (pr * PW + pc) * 64, its 16-B
+//    chunk c stored at c ^ 2 * (pr & 1): with the gfx950 ds_read_b128 lane groups this is
+//    conflict-free for every tap of 2 x 8 and 4 x 4 fragments (checked exhaustively by
+//    tools/halo_conflicts.py), and the row parity of a tap only flips the XOR, so each lane keeps
+//    two bases (even / odd kr). The weight image is the implicit-GEMM kernel's (swz<64>).
+//  * Stages: NST = 1 refills the single stage after a barrier per chunk (two blocks per CU overlap
+//    each other's loads); NST = 2 prefetches chunk k + 1 during chunk k.
+#include "lds_dma.h"
+
+namespace smpq {
+
+struct HaloCfg {
+  int th, tw, nwv, wpf, nst;  // tile rows x cols, waves, pixel fragments per wave, LDS stages
+};
+// tile = th x tw pixels of one image x 64 output channels; ceil(th * tw / 16) == nwv * wpf
+constexpr HaloCfg kHalo[] = {
+    {8, 8, 4, 1, 1},    // 0: 64 px   (56^2; 28^2 with a partial column tile)
+    {16, 8, 8, 1, 1},   // 1: 128 px, 8 waves
+    {16, 8, 4, 2, 1},   // 2: 128 px, 4 waves x 2 fragments
+    {28, 4, 7, 1, 1},   // 3: 112 px  (28^2: whole columns of 4)
+    {14, 4, 4, 1, 1},   // 4: 56 px   (28^2)
+    {8, 8, 4, 1, 2},    // 5: as 0, chunk k + 1 prefetched
+    {28, 4, 7, 1, 2},   // 6: as 3, prefetched
+    {16, 8, 4, 2, 2},   // 7: as 2, prefetched
+    {7, 14, 7, 1, 1},   // 8: 98 px   (14^2: half an image)
+    {7, 14, 7, 1, 2},   // 9: as 8, prefetched
+};
+constexpr int kNumHalo = sizeof(kHalo) / sizeof(kHalo[0]);
+
+namespace {
+
+constexpr int kHaloWB = 9 * 64 * 64;  // weight image per stage: [tap][64 couts][64 B]
+
+__host__ __device__ constexpr int halo_patch_bytes(int L, int th, int tw) {
+  return (L * (th + 2) * (tw + 2) * 64 + 1023) / 1024 * 1024;  // whole DMA pieces
+}
+
+template <int L, int TH, int TW, int NWV, int WPF, int NST>
+__global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nct, int ntw, int tiles_img) {
+  constexpr int PH = TH + 2, PW = TW + 2;
+  constexpr int NPIX = TH * TW;
+  constexpr int NF = NWV * WPF;
+  static_assert(NF * 16 >= NPIX && NF * 16 < NPIX + 16, "fragments cover the tile");
+  constexpr int PLIMB = PH * PW * 64;
+  constexpr int PB = halo_patch_bytes(L, TH, TW);
+  constexpr int STAGE = kHaloWB + PB;
+  constexpr int NPIECE = 36 + PB / 1024;  // 9 taps x 4 weight blocks + the patch
+  constexpr int SLOTS = (NPIECE + NWV - 1) / NWV;
+  extern __shared__ __attribute__((aligned(1024))) int8_t lds[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __builtin_assume(wave >= 0 && wave < NWV);
+  const int frow = lane & 15, grp = lane >> 4;
+
+  // ---- tile: XCD-aware order (consecutive logical tiles share an XCD's L2: the channel tiles of
+  // one patch, then the neighbouring patches whose halos overlap) ------------------------------
+  const int total = gridDim.x, bid = blockIdx.x;
+  const int full = total & ~7;
+  int t = bid;
+  if (t < full) t = (t & 7) * (full >> 3) + (t >> 3);
+  const int ct = t % nct, s = t / nct;
+  const int img = s / tiles_img, rem = s - img * tiles_img;
+  const int tr = rem / ntw, tc = rem - tr * ntw;
+  const int oh0 = tr * TH, ow0 = tc * TW;
+  const int nch = a.cin / 64;
+
+  const v4i wrs = make_rsrc(a.codes, a.wplane);
+  const v4i xrs = make_rsrc(a.xq, (long long)L * a.plane);
+
+  // ---- per-lane DMA sources (fixed over the chunks; the chunk moves the scalar offset) ---------
+  // weight piece p < 36: tap p / 4, couts 16 (p % 4) .. +15 of this channel tile; patch piece q =
+  // p - 36: LDS bytes [1024 q, +1024) of the [L][PH][PW][64] image
+  unsigned src[SLOTS];
+#pragma unroll
+  for (int k = 0; k < SLOTS; ++k) {
+    const int p = wave + NWV * k;
+    unsigned off = kOOB;
+    if (p < 36) {
+      const int tap = p >> 2, i = p & 3;
+      const int row = lane >> 2;
+      const int lc = (lane & 3) ^ swz<64>(row);
+      const int co = ct * 64 + 16 * i + row;
+      off = a.w_kmajor ? (unsigned)(((long long)tap * nch * a.cout + co) * 64 + 16 * lc)
+                       : (unsigned)((long long)co * a.K + tap * a.cin + 16 * lc);
+    } else if (p < NPIECE) {
+      const int sl = 64 * (p - 36) + lane;  // 16-B slot of the patch image
+      const int P = sl >> 2, pc16 = sl & 3;
+      const int l = P / (PH * PW), pp = P - l * (PH * PW);
+      const int pr = pp / PW, pc = pp - pr * PW;
+      const int ih = oh0 + pr - 1, iw = ow0 + pc - 1;
+      const int lc = pc16 ^ (2 * (pr & 1));
+      if (l < L && (unsigned)ih < (unsigned)a.h && (unsigned)iw < (unsigned)a.w)
+        off = (unsigned)((long long)l * a.plane + ((long long)(img * a.h + ih) * a.w + iw) * a.cin + 16 * lc);
+    }
+    src[k] = off;
+  }
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+  const unsigned wchunk = __builtin_amdgcn_readfirstlane(a.w_kmajor ? (unsigned)(a.cout * 64) : 64u);
+  auto issue = [&](int cc, int stage) {
+    const unsigned sb = lds0 + stage * STAGE;
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k) {
+      const int p = wave + NWV * k;
+      if (p < 36)
+        dma16(sb + p * 1024, wrs, src[k], __builtin_amdgcn_readfirstlane((unsigned)cc * wchunk));
+      else if (p < NPIECE)
+        dma16(sb + kHaloWB + (p - 36) * 1024, xrs, src[k], __builtin_amdgcn_readfirstlane((unsigned)cc * 64u));
+    }
+  };
+  constexpr int PPW_MAX = SLOTS;  // pieces this wave issues per chunk (the last wave may issue fewer)
+  int ppw = 0;
+#pragma unroll
+  for (int k = 0; k < SLOTS; ++k) ppw += (wave + NWV * k < NPIECE) ? 1 : 0;
+  (void)PPW_MAX;
+
+  // ---- per-lane fragment bases --------------------------------------------------------------
+  const int wrd = frow * 64 + 16 * (grp ^ swz<64>(frow));  // A: + tap * 4096 + i * 1024
+  int bpar[WPF][2];  // B: + l * PLIMB + (kr * PW + kc) * 64; [1] for odd kr
+  int pr0[WPF], pc0[WPF];
+#pragma unroll
+  for (int j = 0; j < WPF; ++j) {
+    const int pt = 16 * (wave * WPF + j) + frow;
+    const int r = pt < NPIX ? pt / TW : 0, c = pt < NPIX ? pt - (pt / TW) * TW : 0;
+    pr0[j] = pt < NPIX ? r : -1;
+    pc0[j] = c;
+#pragma unroll
+    for (int par = 0; par < 2; ++par) bpar[j][par] = kHaloWB + (r * PW + c) * 64 + 16 * (grp ^ (2 * ((r + par) & 1)));
+  }
+
+  v4i acc[L][4][WPF];
+#pragma unroll
+  for (int l = 0; l < L; ++l)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < WPF; ++j) acc[l][i][j] = v4i{0, 0, 0, 0};
+  const bool do_off = a.has_offset != 0;
+  int rs[L][WPF];
+#pragma unroll
+  for (int l = 0; l < L; ++l)
+#pragma unroll
+    for (int j = 0; j < WPF; ++j) rs[l][j] = 0;
+
+  auto compute = [&](const int8_t* sb) {
+#pragma unroll
+    for (int kr = 0; kr < 3; ++kr)
+#pragma unroll
+      for (int kc = 0; kc < 3; ++kc) {
+        const int tap = kr * 3 + kc;
+        v4i fa[4], fb[L][WPF];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const v4i*>(sb + wrd + tap * 4096 + i * 1024);
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+#pragma unroll
+          for (int j = 0; j < WPF; ++j)
+            fb[l][j] = *reinterpret_cast<const v4i*>(sb + bpar[j][kr & 1] + l * PLIMB + (kr * PW + kc) * 64);
+        if (do_off) {
+#pragma unroll
+          for (int l = 0; l < L; ++l)
+#pragma unroll
+            for (int j = 0; j < WPF; ++j) {
+              int sacc = rs[l][j];
+              sacc = __builtin_amdgcn_sdot4(fb[l][j].x, 0x01010101, sacc, false);
+              sacc = __builtin_amdgcn_sdot4(fb[l][j].y, 0x01010101, sacc, false);
+              sacc = __builtin_amdgcn_sdot4(fb[l][j].z, 0x01010101, sacc, false);
+              sacc = __builtin_amdgcn_sdot4(fb[l][j].w, 0x01010101, sacc, false);
+              rs[l][j] = sacc;
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < WPF; ++j)
+              acc[l][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i], fb[l][j], acc[l][i][j], 0, 0, 0);
+      }
+  };
+
+  if constexpr (NST == 1) {
+    for (int cc = 0; cc < nch; ++cc) {
+      if (cc > 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the last chunk
+        __builtin_amdgcn_s_barrier();                        // ... and every other wave's
+        asm volatile("" ::: "memory");
+      }
+      issue(cc, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      compute(lds);
+    }
+  } else {
+    issue(0, 0);
+    for (int cc = 0; cc < nch; ++cc) {
+      // this wave's DMA of chunk cc has landed (the next one is not issued yet) and its reads of
+      // chunk cc - 1 are done; after the barrier every wave's are: stage cc % 2 is readable and
+      // the other stage (chunk cc - 1's) may be refilled
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (cc + 1 < nch) issue(cc + 1, (cc + 1) & 1);
+      compute(lds + (cc & 1) * STAGE);
+    }
+  }
+  (void)ppw;
+
+  // ---- epilogue: the implicit-GEMM kernel's lean static-range epilogue ------------------------
+  if (do_off) {
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+#pragma unroll
+      for (int j = 0; j < WPF; ++j) {
+        int sacc = rs[l][j];
+        sacc += __shfl_xor(sacc, 16, kWave);
+        sacc += __shfl_xor(sacc, 32, kWave);
+        rs[l][j] = sacc;
+      }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int4 coff = *reinterpret_cast<const int4*>(a.w_off + ct * 64 + 16 * i + 4 * grp);
+      const int cor[4] = {coff.x, coff.y, coff.z, coff.w};
+#pragma unroll
+      for (int l = 0; l < L; ++l)
+#pragma unroll
+        for (int j = 0; j < WPF; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[l][i][j][r] += __mul24(cor[r], rs[l][j]);
+    }
+  }
+  const long long oplane = (long long)a.M * a.cout;
+  unsigned qoff[WPF];
+#pragma unroll
+  for (int j = 0; j < WPF; ++j) {
+    const int oh = oh0 + pr0[j], ow = ow0 + pc0[j];
+    const bool ok = pr0[j] >= 0 && oh < a.ho && ow < a.wo;
+    qoff[j] = ok ? (unsigned)(((long long)(img * a.ho + oh) * a.wo + ow) * a.cout + ct * 64 + 16 * grp) : kOOB;
+  }
+  constexpr float qmax = act_qmax<L>();
+  const float rscale = a.x_absmax[img] * a.inv_qmax;
+  const float inv = a.yq_inv;
+  const float lo = a.relu ? 0.f : -qmax;
+  const bool relu = a.relu != 0;
+  unsigned wq[4][WPF][L];
+  float vmax = 0.f;
+  const int rq_dummy[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = ct * 64 + 16 * i + 4 * grp;
+    const float4 cs = *reinterpret_cast<const float4*>(a.col_scale + c);
+    const float4 csh = *reinterpret_cast<const float4*>(a.col_shift + c);
+    const float csq[4] = {cs.x * inv, cs.y * inv, cs.z * inv, cs.w * inv};
+    const float shq[4] = {csh.x * inv, csh.y * inv, csh.z * inv, csh.w * inv};
+#pragma unroll
+    for (int j = 0; j < WPF; ++j) {
+      v4i accq[L];
+#pragma unroll
+      for (int l = 0; l < L; ++l) accq[l] = acc[l][i][j];
+      const float m = lean_quad<L, L, 0>(accq, rscale, csq, shq, false, rq_dummy, 0.f, relu, lo, wq[i][j]);
+      vmax = qoff[j] != kOOB ? fmaxf(vmax, m) : vmax;
+    }
+  }
+  const v4i qrs4 = make_rsrc(a.yq, (long long)L * oplane);
+  const bool nt = __builtin_amdgcn_readfirstlane(a.nt_store) != 0;
+#pragma unroll
+  for (int j = 0; j < WPF; ++j)
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      unsigned w0 = wq[0][j][l], w1 = wq[1][j][l], w2 = wq[2][j][l], w3 = wq[3][j][l];
+      transpose4(w0, w1, w2, w3);  // lane group g: the 16 channels of block g of its pixel
+      store_limbs16(v4u{w0, w1, w2, w3}, qrs4, qoff[j], __builtin_amdgcn_readfirstlane((unsigned)((long long)l * oplane)),
+                    nt);
+    }
+  if (__any(vmax > qmax) && lane == 0) atomicMax(a.overflow, 1);
+}
+
+template <int L, int TH, int TW, int NWV, int WPF, int NST>
+int launch_halo_one(const ConvArgs& a, hipStream_t stream) {
+  const int nth = (a.ho + TH - 1) / TH, ntw = (a.wo + TW - 1) / TW, nct = a.cout / 64;
+  const long long blocks = (long long)a.n * nth * ntw * nct;
+  if (blocks > 0x7fffffffLL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
+  constexpr int stage = kHaloWB + halo_patch_bytes(L, TH, TW);
+  const int nch = a.cin / 64;
+  const int lds_bytes = (nch < NST ? nch : NST) * stage;
+  constexpr int kMax = NST * stage;
+  static_assert(kMax <= 160 * 1024, "LDS per CU");
+  auto k = qconv_halo_kernel<L, TH, TW, NWV, WPF, NST>;
+  static const hipError_t attr = [&] {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kMax);
+    if (e != hipSuccess) (void)hipGetLastError();
+    return e;
+  }();
+  if (attr != hipSuccess) return check_hip(attr, "qconv_halo_kernel LDS attribute");
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * NWV), lds_bytes, stream, a, nct, ntw, nth * ntw);
+  return check_hip(hipGetLastError(), "qconv_halo_kernel launch");
+}
+
+template <int L>
+int launch_halo_l(int cfg, const ConvArgs& a, hipStream_t s) {
+  switch (cfg) {
+    case 0: return launch_halo_one<L, 8, 8, 4, 1, 1>(a, s);
+    case 1: return launch_halo_one<L, 16, 8, 8, 1, 1>(a, s);
+    case 2: return launch_halo_one<L, 16, 8, 4, 2, 1>(a, s);
+    case 3: return launch_halo_one<L, 28, 4, 7, 1, 1>(a, s);
+    case 4: return launch_halo_one<L, 14, 4, 4, 1, 1>(a, s);
+    case 5: return launch_halo_one<L, 8, 8, 4, 1, 2>(a, s);
+    case 6: return launch_halo_one<L, 28, 4, 7, 1, 2>(a, s);
+    case 7: return launch_halo_one<L, 16, 8, 4, 2, 2>(a, s);
+    case 8: return launch_halo_one<L, 7, 14, 7, 1, 1>(a, s);
+    case 9: return launch_halo_one<L, 7, 14, 7, 1, 2>(a, s);
+    default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad halo tile config");
+  }
+}
+
+}  // namespace
+
+int halo_num_cfgs() { return kNumHalo; }
+
+void halo_cfg_info(int cfg, int* bm, int* bn, int* threads) {
+  const HaloCfg& c = kHalo[cfg];
+  *bm = c.th * c.tw;  // pixels
+  *bn = 64;           // channels
+  *threads = 64 * c.nwv;
+}
+
+// What tile_supported can see: the kernel also needs stride 1, pad 1 and the static-range lean
+// epilogue (limb-plane output only), which the launcher checks.
+bool halo_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs) {
+  (void)cfg;
+  return kh == 3 && kw == 3 && cin % 64 == 0 && cout % 64 == 0 && wlimbs == 1 && limbs >= 2;
+}
+
+int launch_halo(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s) {
+  if (cfg < 0 || cfg >= kNumHalo) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad halo tile config");
+  if (!halo_supported(cfg, a.cin, a.cout, a.kh, a.kw, limbs, wlimbs) || a.stride != 1 || a.pad != 1 || a.s2d)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: halo tiles take 3x3 / stride 1 / pad 1 convs with cin % 64 == 0, "
+                                "cout % 64 == 0 and one weight limb");
+  if (!a.yq || a.y || a.residual || a.res_q || a.y_absmax)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: halo tiles run the static-range limb-plane epilogue only");
+  switch (limbs) {
+    case 2: return launch_halo_l<2>(cfg, a, s);
+    case 3: return launch_halo_l<3>(cfg, a, s);
+    default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: halo tiles need 2 or 3 activation limbs");
+  }
+}
+
+}  // namespace smpq

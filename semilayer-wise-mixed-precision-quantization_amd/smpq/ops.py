@@ -371,12 +371,13 @@ def tile_configs():
     return _TILES
 
 
-TILE_LDS_DMA, TILE_LDS_DMA_K128 = 2, 3  # include/smpq.h SMPQ_TILE_*
+TILE_LDS_DMA, TILE_LDS_DMA_K128, TILE_HALO3X3 = 2, 3, 4  # include/smpq.h SMPQ_TILE_*
 _KINDS = {}
 
 
 def tile_kind(cfg):
-    """Kernel family of a tile config (TILE_LDS_DMA / TILE_LDS_DMA_K128: 64- or 128-wide K steps)."""
+    """Kernel family of a tile config (TILE_LDS_DMA / TILE_LDS_DMA_K128: 64- or 128-wide K steps;
+    TILE_HALO3X3: the halo-patch 3x3 kernel, static-range limb-plane output only)."""
     tile_configs()
     return _KINDS[cfg]
 

@@ -1,0 +1,90 @@
+"""Halo-patch 3x3 kernel (csrc/conv_halo.hip, tile kind TILE_HALO3X3): its static-range limb-plane
+outputs and overflow flags equal the implicit-GEMM kernel's bit for bit on every configuration,
+for full and partial tiles, several input-channel chunks, 2 and 3 activation limbs, weight offsets,
+both weight layouts, ReLU on and off, in range and overflowing. Every call goes through the C-ABI."""
+import pytest
+import torch
+
+from test_gpu import make_layer
+
+pytestmark = pytest.mark.gpu
+
+
+def _halo_cfgs(ops, limbs, cin, cout):
+    return [c for c in ops.tile_configs()
+            if ops.tile_kind(c) == ops.TILE_HALO3X3 and ops._tile_fits(c, limbs, 1, cout, cin, 3)]
+
+
+@pytest.mark.parametrize("relu", [True, False])
+@pytest.mark.parametrize("limbs", [2, 3])
+@pytest.mark.parametrize("shape", [(64, 64, 56, 56, 2), (128, 128, 28, 28, 3), (256, 256, 14, 14, 2),
+                                   (64, 128, 13, 17, 2), (192, 64, 9, 30, 1)],
+                         ids=lambda s: "c%d_o%d_%dx%d_n%d" % s)
+def test_halo_equals_implicit_gemm(gpu, shape, limbs, relu):
+    from smpq import ops
+    cin, cout, h, w, n = shape
+    wd, step, codes, offset = make_layer(gpu, cin, cout, 3, seed=cin + 3 * cout + h)
+    g = torch.Generator().manual_seed(h * w)
+    x = torch.relu(torch.randn(n, h, w, cin, generator=g)).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, limbs)
+    shift = torch.linspace(-1, 1, cout, device=gpu)
+    ref = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=relu)
+    cfgs = _halo_cfgs(ops, limbs, cin, cout)
+    assert cfgs
+    for frac in (2.0, 0.5):
+        rng = float(ref.abs().max()) * frac
+        for layout in ("auto", "rowmajor"):
+            ovf0 = torch.zeros(1, dtype=torch.int32, device=gpu)
+            _, yq0 = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=relu, tile_cfg=-1,
+                                  emit_range=rng, overflow=ovf0, want_f32=False, weight_layout=layout)
+            assert int(ovf0.item()) == (1 if frac < 1 else 0)
+            for c in cfgs:
+                ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+                yq = torch.full_like(yq0, 0x5a)  # every element must be written
+                _, yq = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=relu, tile_cfg=c,
+                                     emit_range=rng, overflow=ovf, want_f32=False, weight_layout=layout)
+                assert torch.equal(yq, yq0), (c, frac, layout)
+                assert torch.equal(ovf, ovf0), (c, frac, layout)
+
+
+def test_halo_without_offsets_and_repeatable(gpu):
+    """No weight offsets (the plain-code path) and 20 back-to-back launches of every halo config
+    give the same bits (no race between the DMA of one chunk and the reads of the last)."""
+    from smpq import ops
+    cin, cout, h = 128, 64, 28
+    wd, step, codes, offset = make_layer(gpu, cin, cout, 3, seed=11, bits_choice=(6, 4))
+    x = torch.relu(torch.randn(4, h, h, cin, generator=torch.Generator().manual_seed(3))).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, 3)
+    shift = torch.zeros(cout, device=gpu)
+    ref = ops.conv2d_q(xq, am, codes, None, 3, 3, 1, 1, step, shift, relu=True)
+    rng = float(ref.abs().max()) * 2
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+    _, yq0 = ops.conv2d_q(xq, am, codes, None, 3, 3, 1, 1, step, shift, relu=True, emit_range=rng, overflow=ovf,
+                          want_f32=False)
+    for c in _halo_cfgs(ops, 3, cin, cout):
+        outs = [ops.conv2d_q(xq, am, codes, None, 3, 3, 1, 1, step, shift, relu=True, tile_cfg=c, emit_range=rng,
+                             overflow=ovf, want_f32=False)[1] for _ in range(20)]
+        for yq in outs:
+            assert torch.equal(yq, yq0), c
+    assert int(ovf.item()) == 0
+
+
+def test_halo_refuses_what_it_does_not_run(gpu):
+    """Stride 2, 1x1, fp32 outputs and residuals are refused with SMPQ_E_INVALID (the autotuner
+    skips such configurations), never run."""
+    from smpq import _lib, ops
+    cin, cout = 64, 64
+    wd, step, codes, offset = make_layer(gpu, cin, cout, 3, seed=5)
+    x = torch.relu(torch.randn(1, 8, 8, cin, generator=torch.Generator().manual_seed(6))).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, 3)
+    shift = torch.zeros(cout, device=gpu)
+    c = _halo_cfgs(ops, 3, cin, cout)[0]
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+    with pytest.raises(_lib.SmpqError, match="halo"):
+        ops.conv2d_q(xq, am, codes, offset, 3, 3, 2, 1, step, shift, tile_cfg=c, emit_range=1.0, overflow=ovf,
+                     want_f32=False)
+    with pytest.raises(_lib.SmpqError, match="halo"):
+        ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, tile_cfg=c)

@@ -10,6 +10,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "semilayer-wise-mixed-precision-quantization_amd"))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tools"))
 import torch  # noqa: E402
 
 import __graft_entry__  # noqa: E402
@@ -20,24 +21,7 @@ from smpq import ops  # noqa: E402
 L, B = 3, int(os.environ.get("TB_BATCH", "256"))
 CFGS = None if len(sys.argv) < 2 or sys.argv[1] == "all" else [int(c) for c in sys.argv[1].split(",")]
 ONLY = sys.argv[2] if len(sys.argv) > 2 else None
-SHAPES = [  # name, cin, cout, k, stride, hin, residual, wlimbs
-    ("c1_256_64_56", 256, 64, 1, 1, 56, False, 1),
-    ("c2_64_64_56", 64, 64, 3, 1, 56, False, 1),
-    ("c3_64_256_56r", 64, 256, 1, 1, 56, True, 1),
-    ("c2_128_128_28", 128, 128, 3, 1, 28, False, 1),
-    ("c2_128_128_56s2", 128, 128, 3, 2, 56, False, 1),
-    ("c1_512_128_28", 512, 128, 1, 1, 28, False, 1),
-    ("c3_128_512_28r", 128, 512, 1, 1, 28, True, 1),
-    ("c2_256_256_14", 256, 256, 3, 1, 14, False, 1),
-    ("c1_1024_256_14", 1024, 256, 1, 1, 14, False, 1),
-    ("c3_256_1024_14r", 256, 1024, 1, 1, 14, True, 1),
-    ("c2_512_512_7", 512, 512, 3, 1, 7, False, 1),
-    ("c1_2048_512_7", 2048, 512, 1, 1, 7, False, 1),
-    ("ds_1024_2048_14s2", 1024, 2048, 1, 2, 14, False, 3),
-    ("ds_512_1024_28s2", 512, 1024, 1, 2, 28, False, 3),
-    ("ds_256_512_56s2", 256, 512, 1, 2, 56, False, 3),
-    ("ds_64_256_56", 64, 256, 1, 1, 56, False, 3),
-]
+from r50_shapes import SHAPES  # noqa: E402
 dev = torch.device("cuda")
 for name, cin, cout, k, s, h, res, wl in SHAPES:
     if ONLY and ONLY not in name:
@@ -64,7 +48,7 @@ for name, cin, cout, k, s, h, res, wl in SHAPES:
     _, ref = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, wscale, shift, tile_cfg=-1, **kw)
     out = []
     for c in ops.tile_configs():
-        if ops.tile_kind(c) not in (ops.TILE_LDS_DMA, ops.TILE_LDS_DMA_K128):
+        if ops.tile_kind(c) not in (ops.TILE_LDS_DMA, ops.TILE_LDS_DMA_K128, ops.TILE_HALO3X3):
             continue
         if not ops._tile_fits(c, L, wl, cout, cin, k) or (CFGS is not None and c not in CFGS):
             continue
