@@ -67,13 +67,18 @@ __device__ unsigned long long* smpq_stamps;
 // NST LDS stages: the DMA of K step k + NST - 1 is in flight while step k computes.
 // BK: K bytes per stage and row. 64 = one MFMA K; 128 (cin % 128 == 0) = two, and every DMA piece
 // is then 8 whole 128-B lines instead of 16 half lines (half the TA/TD work per byte).
-// LEAN: the static-range epilogue that only emits the next conv's limb planes (no fp32 output, no
+// LEAN (0: the general epilogue; 1: lean, ReLU and residual decided at run time; 2: lean with
+// ReLU, no residual — conv1 / conv2; 3: lean with ReLU and a limb-plane residual — conv3): the
+// static-range epilogue that only emits the next conv's limb planes (no fp32 output, no
 // fp32 residual, no per-image maxima): the output quantizer's 1/step is folded into the column
 // scale / shift and the residual scale, ReLU and the code clamp are one v_med3, and overflow is
 // tracked on the rounded codes — about half the VALU work of the general epilogue per output.
 // The body of one block (block `bid` of `total` blocks of this conv); `lds` = the dynamic LDS.
+// OFF: weight offsets may be present (a.has_offset decides at run time); instantiated without them
+// the offset sums and their correction compile away (a runtime-false branch still cost the
+// epilogue ~50 register moves per wave to merge the two paths' accumulators).
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
-          bool LEAN = false, bool PIPE = false>
+          int LEAN = 0, bool PIPE = false, bool OFF = true>
 __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, int8_t* lds) {
   static_assert(BK == 64 || BK == 128, "BK");
   static_assert(!S2D || BK == 64, "the s2d stem uses 64-B K steps");
@@ -207,7 +212,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     for (int i = 0; i < WC; ++i)
 #pragma unroll
       for (int j = 0; j < WP; ++j) acc[s][i][j] = v4i{0, 0, 0, 0};
-  const bool do_off = (LW == 1) && a.has_offset;
+  const bool do_off = OFF && (LW == 1) && a.has_offset;
   int rs[L][WP];  // per-lane partial pixel sums of activation codes (LW == 1 offset correction)
 #pragma unroll
   for (int l = 0; l < L; ++l)
@@ -249,7 +254,9 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   constexpr bool TR = TRT;
   constexpr int NQ = TR ? WC / 4 : 1;
   const bool lines = (kAblate & 32) ? BC >= 128 : (BC >= 128 || BC == a.cout);
-  const bool stage_res = TR && a.res_q && lines, stage_out = TR && a.yq && lines;
+  // limb-plane residual (compile-time in the LEAN 2 / 3 variants: no merged paths in the epilogue)
+  const bool has_rq = LEAN == 3 || (LEAN != 2 && a.res_q != nullptr);
+  const bool stage_res = TR && has_rq && lines, stage_out = TR && a.yq && lines;
   unsigned qoff[NQ][WP];
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
@@ -264,7 +271,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   const int nst_eff = nsteps < NST ? nsteps : NST;
   const int resoff = (stage_out && TILEB > nst_eff * STAGE) ? TILEB : nst_eff * STAGE;  // LDS layout
   if constexpr (TR) {
-    if (a.res_q && !stage_res) {
+    if (has_rq && !stage_res) {
       const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.res_q), 0, (int)(L * oplane),
                                                          0x00020000);
 #pragma unroll
@@ -279,7 +286,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 #pragma unroll
             for (int c = 0; c < 4; ++c) rq[4 * q + c][j][l] = (int)v[c];
           }
-    } else if (a.res_q) {
+    } else if (has_rq) {
       // the [L][BP][BC] tile by LDS-DMA: piece = 1024 / BC rows of BC bytes
       constexpr int RROWS = 1024 / BC, RCPR = BC / 16, RPL = BP * BC / 1024, RPIECES = L * RPL;
       const v4i rrs = make_rsrc(a.res_q, (long long)L * oplane);
@@ -297,7 +304,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
         }
       }
     }
-  } else if (a.res_q) {
+  } else if (has_rq) {
     const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.res_q), 0, (int)(L * oplane),
                                                        0x00020000);
 #pragma unroll
@@ -514,7 +521,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     return base + l * BP * BC + rt * BC + 16 * (cc ^ swze<BC>(frow)) + 4 * (lane >> 4);
   };
   if constexpr (TR) {
-    if (a.res_q && !stage_res) {
+    if (has_rq && !stage_res) {
       // lane (g, p) loaded 16 channels of block 4q + g: transpose to the accumulator layout
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
@@ -564,7 +571,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   for (int j = 0; j < WP; ++j) rscale[j] = mok[j] ? a.x_absmax[fast_div(mrow[j], a.hw_mul, a.hw_shr)] * a.inv_qmax : 0.f;
   // residual limb planes -> codes, all at once (one LDS wait instead of one per block)
   int rqv[WC][WP][4];
-  if (a.res_q) {
+  if (has_rq) {
     unsigned rw[WC][WP][L];
 #pragma unroll
     for (int i = 0; i < WC; ++i)
@@ -603,9 +610,9 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     // register pairs and cost more moves than they save here.
     const float inv = a.yq_inv;
     const float rsq = a.res_scale * inv;
-    const float lo = a.relu ? 0.f : -qmax;
-    const bool has_res = a.res_q != nullptr;
-    const bool relu = a.relu != 0;
+    const bool relu = LEAN >= 2 || a.relu != 0;
+    const float lo = relu ? 0.f : -qmax;
+    const bool has_res = has_rq;
 #pragma unroll
     for (int i = 0; i < WC; ++i) {
       const int c = chan[i] < a.cout ? chan[i] : 0;
@@ -638,14 +645,14 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
         for (int h = 0; h < 2; ++h) {
           const f2 sc = f2{rscale[j], rscale[j]} * csr[h];
           f2 out = __builtin_elementwise_fma(combine(i, j, h), sc, shr[h]);
-          if (a.res_q)
+          if (has_rq)
             out = out + f2{a.res_scale, a.res_scale} * f2{(float)rqv[i][j][2 * h], (float)rqv[i][j][2 * h + 1]};
           o[i][j][2 * h] = out.x;
           o[i][j][2 * h + 1] = out.y;
         }
       }
     }
-    if (a.residual && !a.res_q) {
+    if (a.residual && !has_rq) {
       const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.residual), 0, (int)(4 * oplane),
                                                          0x00020000);
       v4u rv[WC][WP];
@@ -799,10 +806,10 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 }
 
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
-          bool LEAN = false, bool PIPE = false>
+          int LEAN = 0, bool PIPE = false, bool OFF = true>
 __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // min(NST, ksteps) stages
-  qconv_glds_body<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, LEAN, PIPE>(a, blockIdx.x, gridDim.x, lds);
+  qconv_glds_body<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, LEAN, PIPE, OFF>(a, blockIdx.x, gridDim.x, lds);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -886,20 +893,37 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
     ConvArgs b = a;
     fast_div_init((int)nt, b.ntc_mul, b.ntc_shr);
     const bool lean = L >= 2 && a.yq && !a.y && !a.residual && !a.y_absmax;
-    auto kfull = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, false, PIPE>;
-    auto klean = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, (L >= 2), PIPE>;
+    // epilogue variants: general / lean (runtime ReLU + residual) / lean ReLU / lean ReLU + limb-plane
+    // residual, each with and without weight offsets (LW == 1 only; the compile-time ReLU and
+    // residual variants too: the block convs of the quantized ResNets)
+    constexpr bool kV = LW == 1 && L >= 2;
+    constexpr int kLean = L >= 2 ? 1 : 0;
+    auto k00 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, 0, PIPE, false>;
+    auto k10 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kLean, PIPE, false>;
+    auto k20 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 2 : kLean, PIPE, false>;
+    auto k30 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 3 : kLean, PIPE, false>;
+    auto k01 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, 0, PIPE, LW == 1>;
+    auto k11 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kLean, PIPE, LW == 1>;
+    auto k21 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 2 : kLean, PIPE, LW == 1>;
+    auto k31 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 3 : kLean, PIPE, LW == 1>;
     auto set_lds = [](const void* k) {
       const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                kMaxNeed < kMaxLds ? kMaxNeed : kMaxLds);
       if (e != hipSuccess) (void)hipGetLastError();  // do not leave it for an unrelated launch to report
       return e;
     };
-    static const hipError_t attr_full = set_lds(reinterpret_cast<const void*>(kfull));
-    static const hipError_t attr_lean = set_lds(reinterpret_cast<const void*>(klean));
-    const hipError_t attr = lean ? attr_lean : attr_full;
-    if (attr != hipSuccess) return check_hip(attr, "qconv_glds_kernel LDS attribute");
-    hipLaunchKernelGGL(lean ? klean : kfull, dim3((unsigned)(mt * nt)), dim3(64 * WAVES_C * WAVES_P), lds_bytes,
-                       stream, b);
+    using KFn = decltype(k00);
+    static const KFn fns[8] = {k00, k10, k20, k30, k01, k11, k21, k31};
+    static hipError_t attrs[8];
+    static const bool attrs_set = [&] {
+      for (int i = 0; i < 8; ++i) attrs[i] = set_lds(reinterpret_cast<const void*>(fns[i]));
+      return true;
+    }();
+    (void)attrs_set;
+    const int ev = !lean ? 0 : (!kV || !a.relu) ? 1 : (a.res_q ? 3 : 2);
+    const int vi = ev + ((LW == 1 && a.has_offset) ? 4 : 0);
+    if (attrs[vi] != hipSuccess) return check_hip(attrs[vi], "qconv_glds_kernel LDS attribute");
+    hipLaunchKernelGGL(fns[vi], dim3((unsigned)(mt * nt)), dim3(64 * WAVES_C * WAVES_P), lds_bytes, stream, b);
     return check_hip(hipGetLastError(), "qconv_glds_kernel launch");
   }
 }

@@ -24,6 +24,8 @@
 //    two bases (even / odd kr). The weight image is the implicit-GEMM kernel's (swz<64>).
 //  * Stages: NST = 1 refills the single stage after a barrier per chunk (two blocks per CU overlap
 //    each other's loads); NST = 2 prefetches chunk k + 1 during chunk k.
+#include <type_traits>
+
 #include "lds_dma.h"
 
 namespace smpq {
@@ -54,7 +56,7 @@ __host__ __device__ constexpr int halo_patch_bytes(int L, int th, int tw) {
   return (L * (th + 2) * (tw + 2) * 64 + 1023) / 1024 * 1024;  // whole DMA pieces
 }
 
-template <int L, int TH, int TW, int NWV, int WPF, int NST>
+template <int L, int TH, int TW, int NWV, int WPF, int NST, bool OFF>
 __global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nct, int ntw, int tiles_img) {
   constexpr int PH = TH + 2, PW = TW + 2;
   constexpr int NPIX = TH * TW;
@@ -63,8 +65,8 @@ __global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nc
   constexpr int PLIMB = PH * PW * 64;
   constexpr int PB = halo_patch_bytes(L, TH, TW);
   constexpr int STAGE = kHaloWB + PB;
-  constexpr int NPIECE = 36 + PB / 1024;  // 9 taps x 4 weight blocks + the patch
-  constexpr int SLOTS = (NPIECE + NWV - 1) / NWV;
+  constexpr int PPIECE = PB / 1024;       // patch pieces; + 9 taps x 4 blocks of 16 couts of weights
+  constexpr int WSL = (36 + NWV - 1) / NWV, PSL = (PPIECE + NWV - 1) / NWV;
   extern __shared__ __attribute__((aligned(1024))) int8_t lds[];
 
   const int lane = threadIdx.x & 63;
@@ -88,50 +90,68 @@ __global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nc
   const v4i xrs = make_rsrc(a.xq, (long long)L * a.plane);
 
   // ---- per-lane DMA sources (fixed over the chunks; the chunk moves the scalar offset) ---------
-  // weight piece p < 36: tap p / 4, couts 16 (p % 4) .. +15 of this channel tile; patch piece q =
-  // p - 36: LDS bytes [1024 q, +1024) of the [L][PH][PW][64] image
-  unsigned src[SLOTS];
+  // weight piece p = wave + NWV k (< 36): tap p / 4, couts 16 (p % 4) .. +15 of this channel tile;
+  // patch piece q = wave + NWV k (< PPIECE): LDS bytes [1024 q, +1024) of the [L][PH][PW][64]
+  // image, i.e. pixels 16 q .. 16 q + 15 (4 lanes per pixel). Patch coordinates advance
+  // incrementally from piece to piece (no division per piece); offsets are 32-bit (every operand
+  // plane is below 2 GiB, glds_planes_ok).
+  unsigned wsrc[WSL], psrc[PSL];
+  {
+    const int row = lane >> 2;
+    const int lc = (lane & 3) ^ swz<64>(row);
+    const unsigned rowoff = a.w_kmajor ? (unsigned)((ct * 64 + row) * 64 + 16 * lc)
+                                       : (unsigned)((ct * 64 + row) * a.K + 16 * lc);
+    const unsigned tapstride = a.w_kmajor ? (unsigned)(nch * a.cout * 64) : (unsigned)a.cin;
+    const unsigned blkstride = a.w_kmajor ? 16u * 64u : 16u * (unsigned)a.K;
 #pragma unroll
-  for (int k = 0; k < SLOTS; ++k) {
-    const int p = wave + NWV * k;
-    unsigned off = kOOB;
-    if (p < 36) {
-      const int tap = p >> 2, i = p & 3;
-      const int row = lane >> 2;
-      const int lc = (lane & 3) ^ swz<64>(row);
-      const int co = ct * 64 + 16 * i + row;
-      off = a.w_kmajor ? (unsigned)(((long long)tap * nch * a.cout + co) * 64 + 16 * lc)
-                       : (unsigned)((long long)co * a.K + tap * a.cin + 16 * lc);
-    } else if (p < NPIECE) {
-      const int sl = 64 * (p - 36) + lane;  // 16-B slot of the patch image
-      const int P = sl >> 2, pc16 = sl & 3;
-      const int l = P / (PH * PW), pp = P - l * (PH * PW);
-      const int pr = pp / PW, pc = pp - pr * PW;
-      const int ih = oh0 + pr - 1, iw = ow0 + pc - 1;
-      const int lc = pc16 ^ (2 * (pr & 1));
-      if (l < L && (unsigned)ih < (unsigned)a.h && (unsigned)iw < (unsigned)a.w)
-        off = (unsigned)((long long)l * a.plane + ((long long)(img * a.h + ih) * a.w + iw) * a.cin + 16 * lc);
+    for (int k = 0; k < WSL; ++k) {
+      const int p = wave + NWV * k;
+      wsrc[k] = p < 36 ? rowoff + (unsigned)(p >> 2) * tapstride + (unsigned)(p & 3) * blkstride : kOOB;
     }
-    src[k] = off;
+  }
+  {
+    constexpr int D = 16 * NWV;                     // pixels between a wave's consecutive pieces
+    constexpr int DL = D / (PH * PW), DR = (D % (PH * PW)) / PW, DC = D % PW;
+    int P = 16 * wave + (lane >> 2);                // this lane's pixel in the wave's first piece
+    int l = P / (PH * PW);
+    int pr = (P - l * (PH * PW)) / PW;
+    int pc = P - l * (PH * PW) - pr * PW;
+    const int c16 = 16 * (lane & 3);
+    const int wcin = a.w * a.cin;
+    const int q0 = ((img * a.h + oh0 - 1) * a.w + ow0 - 1) * a.cin;  // patch pixel (0, 0); may be < 0
+    const int h1 = a.h - oh0 + 1, w1 = a.w - ow0 + 1;               // pr < h1 <=> ih < h
+    const unsigned plane = (unsigned)a.plane;
+#pragma unroll
+    for (int k = 0; k < PSL; ++k) {
+      const int q = wave + NWV * k;
+      const bool ok = q < PPIECE && l < L && pr >= 1 - oh0 && pr < h1 && pc >= 1 - ow0 && pc < w1;
+      psrc[k] = ok ? (unsigned)l * plane + (unsigned)(q0 + pr * wcin + pc * a.cin + (c16 ^ (32 * (pr & 1)))) : kOOB;
+      pc += DC;
+      pr += DR;
+      if (pc >= PW) {
+        pc -= PW;
+        ++pr;
+      }
+      l += DL;
+      if (pr >= PH) {
+        pr -= PH;
+        ++l;
+      }
+    }
   }
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   const unsigned wchunk = __builtin_amdgcn_readfirstlane(a.w_kmajor ? (unsigned)(a.cout * 64) : 64u);
   auto issue = [&](int cc, int stage) {
     const unsigned sb = lds0 + stage * STAGE;
 #pragma unroll
-    for (int k = 0; k < SLOTS; ++k) {
-      const int p = wave + NWV * k;
-      if (p < 36)
-        dma16(sb + p * 1024, wrs, src[k], __builtin_amdgcn_readfirstlane((unsigned)cc * wchunk));
-      else if (p < NPIECE)
-        dma16(sb + kHaloWB + (p - 36) * 1024, xrs, src[k], __builtin_amdgcn_readfirstlane((unsigned)cc * 64u));
-    }
-  };
-  constexpr int PPW_MAX = SLOTS;  // pieces this wave issues per chunk (the last wave may issue fewer)
-  int ppw = 0;
+    for (int k = 0; k < WSL; ++k)
+      if (wave + NWV * k < 36)
+        dma16(sb + (wave + NWV * k) * 1024, wrs, wsrc[k], __builtin_amdgcn_readfirstlane((unsigned)cc * wchunk));
 #pragma unroll
-  for (int k = 0; k < SLOTS; ++k) ppw += (wave + NWV * k < NPIECE) ? 1 : 0;
-  (void)PPW_MAX;
+    for (int k = 0; k < PSL; ++k)
+      if (wave + NWV * k < PPIECE)
+        dma16(sb + kHaloWB + (wave + NWV * k) * 1024, xrs, psrc[k], __builtin_amdgcn_readfirstlane((unsigned)cc * 64u));
+  };
 
   // ---- per-lane fragment bases --------------------------------------------------------------
   const int wrd = frow * 64 + 16 * (grp ^ swz<64>(frow));  // A: + tap * 4096 + i * 1024
@@ -147,21 +167,15 @@ __global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nc
     for (int par = 0; par < 2; ++par) bpar[j][par] = kHaloWB + (r * PW + c) * 64 + 16 * (grp ^ (2 * ((r + par) & 1)));
   }
 
-  v4i acc[L][4][WPF];
-#pragma unroll
-  for (int l = 0; l < L; ++l)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < WPF; ++j) acc[l][i][j] = v4i{0, 0, 0, 0};
-  const bool do_off = a.has_offset != 0;
+  v4i acc[L][4][WPF];  // set by the first chunk's first tap (an MFMA with a zero C operand)
+  constexpr bool do_off = OFF;  // weight offsets (compile-time: no merged paths in the epilogue)
   int rs[L][WPF];
 #pragma unroll
   for (int l = 0; l < L; ++l)
 #pragma unroll
     for (int j = 0; j < WPF; ++j) rs[l][j] = 0;
 
-  auto compute = [&](const int8_t* sb) {
+  auto compute = [&](const int8_t* sb, auto first) {
 #pragma unroll
     for (int kr = 0; kr < 3; ++kr)
 #pragma unroll
@@ -175,7 +189,7 @@ __global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nc
 #pragma unroll
           for (int j = 0; j < WPF; ++j)
             fb[l][j] = *reinterpret_cast<const v4i*>(sb + bpar[j][kr & 1] + l * PLIMB + (kr * PW + kc) * 64);
-        if (do_off) {
+        if constexpr (do_off) {
 #pragma unroll
           for (int l = 0; l < L; ++l)
 #pragma unroll
@@ -194,40 +208,50 @@ __global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nc
           for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < WPF; ++j)
-              acc[l][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i], fb[l][j], acc[l][i][j], 0, 0, 0);
+              acc[l][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                  fa[i], fb[l][j], (decltype(first)::value && tap == 0) ? v4i{0, 0, 0, 0} : acc[l][i][j], 0, 0, 0);
       }
   };
 
+  using First = std::integral_constant<bool, true>;
+  using Later = std::integral_constant<bool, false>;
   if constexpr (NST == 1) {
-    for (int cc = 0; cc < nch; ++cc) {
-      if (cc > 0) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the last chunk
-        __builtin_amdgcn_s_barrier();                        // ... and every other wave's
-        asm volatile("" ::: "memory");
-      }
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    compute(lds, First{});
+    for (int cc = 1; cc < nch; ++cc) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the last chunk
+      __builtin_amdgcn_s_barrier();                        // ... and every other wave's
+      asm volatile("" ::: "memory");
       issue(cc, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      compute(lds);
+      compute(lds, Later{});
     }
   } else {
+    // at the top of chunk cc: this wave's DMA of chunk cc has landed (chunk cc + 1 is not issued
+    // yet) and its reads of chunk cc - 1 are done; after the barrier every wave's are, so stage
+    // cc % 2 is readable and the other stage (chunk cc - 1's) may be refilled
     issue(0, 0);
-    for (int cc = 0; cc < nch; ++cc) {
-      // this wave's DMA of chunk cc has landed (the next one is not issued yet) and its reads of
-      // chunk cc - 1 are done; after the barrier every wave's are: stage cc % 2 is readable and
-      // the other stage (chunk cc - 1's) may be refilled
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (nch > 1) issue(1, 1);
+    compute(lds, First{});
+    for (int cc = 1; cc < nch; ++cc) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (cc + 1 < nch) issue(cc + 1, (cc + 1) & 1);
-      compute(lds + (cc & 1) * STAGE);
+      compute(lds + (cc & 1) * STAGE, Later{});
     }
   }
-  (void)ppw;
 
   // ---- epilogue: the implicit-GEMM kernel's lean static-range epilogue ------------------------
-  if (do_off) {
+  if constexpr (do_off) {
 #pragma unroll
     for (int l = 0; l < L; ++l)
 #pragma unroll
@@ -260,8 +284,8 @@ __global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nc
   constexpr float qmax = act_qmax<L>();
   const float rscale = a.x_absmax[img] * a.inv_qmax;
   const float inv = a.yq_inv;
-  const float lo = a.relu ? 0.f : -qmax;
-  const bool relu = a.relu != 0;
+  constexpr float lo = 0.f;  // ReLU (compile-time: the 3x3 convs of the ResNets; the launcher checks)
+  constexpr bool relu = true;
   unsigned wq[4][WPF][L];
   float vmax = 0.f;
   const int rq_dummy[4] = {0, 0, 0, 0};
@@ -305,14 +329,18 @@ int launch_halo_one(const ConvArgs& a, hipStream_t stream) {
   const int lds_bytes = (nch < NST ? nch : NST) * stage;
   constexpr int kMax = NST * stage;
   static_assert(kMax <= 160 * 1024, "LDS per CU");
-  auto k = qconv_halo_kernel<L, TH, TW, NWV, WPF, NST>;
-  static const hipError_t attr = [&] {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, kMax);
+  auto k0 = qconv_halo_kernel<L, TH, TW, NWV, WPF, NST, false>;
+  auto k1 = qconv_halo_kernel<L, TH, TW, NWV, WPF, NST, true>;
+  auto set_lds = [](const void* k) {
+    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kMax);
     if (e != hipSuccess) (void)hipGetLastError();
     return e;
-  }();
-  if (attr != hipSuccess) return check_hip(attr, "qconv_halo_kernel LDS attribute");
+  };
+  static const hipError_t attr0 = set_lds(reinterpret_cast<const void*>(k0));
+  static const hipError_t attr1 = set_lds(reinterpret_cast<const void*>(k1));
+  const bool off = a.has_offset != 0;
+  if ((off ? attr1 : attr0) != hipSuccess) return check_hip(off ? attr1 : attr0, "qconv_halo_kernel LDS attribute");
+  auto k = off ? k1 : k0;
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * NWV), lds_bytes, stream, a, nct, ntw, nth * ntw);
   return check_hip(hipGetLastError(), "qconv_halo_kernel launch");
 }
@@ -357,8 +385,8 @@ int launch_halo(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s
   if (!halo_supported(cfg, a.cin, a.cout, a.kh, a.kw, limbs, wlimbs) || a.stride != 1 || a.pad != 1 || a.s2d)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: halo tiles take 3x3 / stride 1 / pad 1 convs with cin % 64 == 0, "
                                 "cout % 64 == 0 and one weight limb");
-  if (!a.yq || a.y || a.residual || a.res_q || a.y_absmax)
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: halo tiles run the static-range limb-plane epilogue only");
+  if (!a.yq || a.y || a.residual || a.res_q || a.y_absmax || !a.relu)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: halo tiles run the static-range limb-plane epilogue with ReLU only");
   switch (limbs) {
     case 2: return launch_halo_l<2>(cfg, a, s);
     case 3: return launch_halo_l<3>(cfg, a, s);

@@ -21,7 +21,7 @@ def _halo_cfgs(ops, limbs, cin, cout):
                                    (64, 128, 13, 17, 2), (192, 64, 9, 30, 1)],
                          ids=lambda s: "c%d_o%d_%dx%d_n%d" % s)
 def test_halo_equals_implicit_gemm(gpu, shape, limbs, relu):
-    from smpq import ops
+    from smpq import _lib, ops
     cin, cout, h, w, n = shape
     wd, step, codes, offset = make_layer(gpu, cin, cout, 3, seed=cin + 3 * cout + h)
     g = torch.Generator().manual_seed(h * w)
@@ -41,6 +41,11 @@ def test_halo_equals_implicit_gemm(gpu, shape, limbs, relu):
             assert int(ovf0.item()) == (1 if frac < 1 else 0)
             for c in cfgs:
                 ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+                if not relu:  # the halo kernel runs the ReLU convs only (the autotuner skips it here)
+                    with pytest.raises(_lib.SmpqError, match="halo"):
+                        ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=relu, tile_cfg=c,
+                                     emit_range=rng, overflow=ovf, want_f32=False, weight_layout=layout)
+                    continue
                 yq = torch.full_like(yq0, 0x5a)  # every element must be written
                 _, yq = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=relu, tile_cfg=c,
                                      emit_range=rng, overflow=ovf, want_f32=False, weight_layout=layout)
@@ -72,7 +77,7 @@ def test_halo_without_offsets_and_repeatable(gpu):
 
 
 def test_halo_refuses_what_it_does_not_run(gpu):
-    """Stride 2, 1x1, fp32 outputs and residuals are refused with SMPQ_E_INVALID (the autotuner
+    """Stride 2, fp32 outputs and no-ReLU convs are refused with SMPQ_E_INVALID (the autotuner
     skips such configurations), never run."""
     from smpq import _lib, ops
     cin, cout = 64, 64

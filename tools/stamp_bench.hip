@@ -78,7 +78,7 @@ int run(int argc, char** argv) {
   printf("{\"shape\": \"%dx%d/%d %d->%d at %d^2, B=%d, BK=%d, LW=%d, ablate=%d\", \"kernel_us\": ", k, k, stride, cin, cout,
          hw, n, BK, LW, SMPQ_DIAG_ABLATE);
 #endif
-  auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, 2, false, NST, BK, true, false>;
+  auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, 2, false, NST, BK, 1, false>;
   const int nsteps = a.ksteps / (BK / 64);
   const int lds = std::min(nsteps, NST) * STAGE;
   CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
