@@ -248,8 +248,8 @@ def test_all_tile_configs_bitwise_identical(gpu, shape, limbs):
     res = torch.randn(3, ho, ho, cout, generator=torch.Generator().manual_seed(10)).to(gpu)
     shift = torch.linspace(-1, 1, cout, device=gpu)
     outs = []
-    for c in ops.tile_configs():
-        if not ops._tile_fits(c, limbs, 1, cout, cin, k):
+    for c in ops.tile_configs():  # (the halo kernel runs the lean epilogue only: test_gpu_halo.py)
+        if not ops._tile_fits(c, limbs, 1, cout, cin, k) or ops.tile_kind(c) == ops.TILE_HALO3X3:
             continue
         ya = torch.zeros(3, device=gpu)
         y = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, residual=res, relu=True,
@@ -287,7 +287,7 @@ def test_static_outputs_identical_across_tiles(gpu, shape, limbs, range_frac):
     rng = float(ref.abs().max()) * range_frac
     outs = []
     for c in ops.tile_configs():
-        if not ops._tile_fits(c, limbs, 1, cout, cin, k):
+        if not ops._tile_fits(c, limbs, 1, cout, cin, k) or ops.tile_kind(c) == ops.TILE_HALO3X3:
             continue
         ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
         y, yq = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, relu=True, tile_cfg=c,
@@ -638,7 +638,7 @@ def test_conv_weight_limbs_vs_emulation(gpu, limbs, wlimbs):
     outs = []
     kinds = set()
     for c in ops.tile_configs():
-        if ops._tile_fits(c, limbs, wlimbs, cout, cin, k):
+        if ops._tile_fits(c, limbs, wlimbs, cout, cin, k) and ops.tile_kind(c) != ops.TILE_HALO3X3:
             outs.append(ops.conv2d_q(xq, am, codes, None, k, k, s, 1, cs, sh, residual=res, relu=True, tile_cfg=c))
             kinds.add(ops.tile_kind(c))
     assert ops.TILE_LDS_DMA in kinds and ops.TILE_LDS_DMA_K128 in kinds
@@ -1045,7 +1045,8 @@ def test_tile_configs_deterministic(gpu, shape):
     ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
     y0, q0 = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, tile_cfg=1, emit_range=rng,
                           overflow=ovf, **kw)
-    cfgs = [c for c in ops.tile_configs() if ops._tile_fits(c, limbs, 1, cout, cin, k)]
+    cfgs = [c for c in ops.tile_configs() if ops._tile_fits(c, limbs, 1, cout, cin, k)
+            and ops.tile_kind(c) != ops.TILE_HALO3X3]  # (fp32 output + residual: not the halo kernel's)
     for c in cfgs:
         for rep in range(8):
             y, q = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, tile_cfg=c, emit_range=rng,
