@@ -119,7 +119,7 @@ class ConvTimer:
         return {
             "bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": None,
-            "kernel": "quantized conv (qconv_glds_kernel + qconv_stem_pool_kernel), all launches incl. the stem",
+            "kernel": "quantized conv (qconv_glds_kernel + qconv_halo_kernel + qconv_stem_pool_kernel), all launches incl. the stem",
             "launches_per_step": n // max(steps, 1),
             "avg_launch_ms": round(t_sum / max(n, 1) * 1e3, 5),
             "alg_bytes_per_launch": round(nbytes / max(n, 1)),
