@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Join tools/pmc_layers.sh's two PMC passes to bench.py's layer table: per quantized-conv launch of
+the eager roofline region (the last 53 x 3 dispatches), the instruction mix per wave (VALU, SALU,
+LDS, VMEM) against its MFMA cycles, and the wave states. Diagnostics only.
+
+usage: python tools/pmc_layers.py <outdir>"""
+import csv
+import glob
+import os
+import re
+import sys
+
+O = sys.argv[1]
+N, R = 53, 3
+
+
+def load(d):
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+    rows = {}
+    for r in csv.DictReader(open(f)):
+        if "qconv" not in r["Kernel_Name"]:
+            continue
+        k = int(r["Dispatch_Id"])
+        rows.setdefault(k, {"name": r["Kernel_Name"], "vgpr": r["VGPR_Count"], "agpr": r["Accum_VGPR_Count"]})
+        rows[k][r["Counter_Name"]] = rows[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return [rows[k] for k in sorted(rows)][-N * R:]
+
+
+p1, p2 = load(os.path.join(O, "p1")), load(os.path.join(O, "p2"))
+layers = []
+log = open(os.path.join(O, "p1.log")).read().splitlines()
+try:
+    i = next(j for j, l in enumerate(log) if l.startswith("launch"))
+    layers = [l[:33] + l[33:43] for l in log[i + 1:i + 1 + N]]
+except StopIteration:
+    layers = [""] * N
+print("%-43s %5s %7s %6s %6s %6s %6s %5s %5s %5s %5s %6s" % (
+    "launch (t_us)", "vgpr", "waves", "VALU/w", "SALU/w", "LDS/w", "MFMAc/w", "V/MF", "wait", "istl", "actv", "mfma%"))
+for j in range(N):
+    a = [p1[r * N + j] for r in range(R)]
+    b = [p2[r * N + j] for r in range(R)]
+    def m(lst, k):
+        return sum(x.get(k, 0.0) for x in lst) / len(lst)
+    w = m(a, "SQ_WAVES")
+    mf = m(a, "SQ_VALU_MFMA_BUSY_CYCLES")
+    wc = m(b, "SQ_WAIT_ANY") + m(b, "SQ_WAIT_INST_ANY") + m(b, "SQ_ACTIVE_INST_ANY")
+    gui = m(b, "GRBM_GUI_ACTIVE")
+    print("%-43s %5s %7d %6.0f %6.0f %6.0f %6.0f %5.2f %5.2f %5.2f %5.2f %6.1f" % (
+        layers[j] if j < len(layers) else "", a[0]["vgpr"], w, m(a, "SQ_INSTS_VALU") / w, m(a, "SQ_INSTS_SALU") / w,
+        m(a, "SQ_INSTS_LDS") / w, mf / w, m(a, "SQ_INSTS_VALU") / max(mf / 16, 1),
+        m(b, "SQ_WAIT_ANY") / wc, m(b, "SQ_WAIT_INST_ANY") / wc, m(b, "SQ_ACTIVE_INST_ANY") / wc,
+        100 * mf / max(gui * 128, 1)))
