@@ -51,9 +51,16 @@ constexpr int kAblate = SMPQ_DIAG_ABLATE;
 // wave, vector stores); the product library never defines SMPQ_STAMPS.
 #ifdef SMPQ_STAMPS
 __device__ unsigned long long* smpq_stamps;
-#define SMPQ_STAMP(slot)                                                                                \
-  do {                                                                                                  \
-    if (lane == 0) smpq_stamps[((size_t)bid * NW + wave) * 32 + (slot)] = __builtin_amdgcn_s_memtime(); \
+// The stamp buffer's address is read once per wave (stamp_base, at kernel start), and each stamp is
+// a plain global store issued without waiting: a per-stamp load of the pointer would make every
+// stamp wait (vmcnt) for the previous stamp's store to complete, ~2-3k cycles each.
+#define SMPQ_STAMP(slot)                                                                                    \
+  do {                                                                                                      \
+    if (lane == 0) {                                                                                        \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                         \
+      unsigned long long* p_ = stamp_base + (slot);                                                         \
+      asm volatile("global_store_dwordx2 %0, %1, off\n\ts_nop 1" ::"v"(p_), "v"(t_) : "memory");            \
+    }                                                                                                       \
   } while (0)
 #else
 #define SMPQ_STAMP(slot) \
@@ -109,6 +116,9 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifdef SMPQ_STAMPS
+  unsigned long long* const stamp_base = smpq_stamps + ((size_t)bid * NW + wave) * 32;
+#endif
   SMPQ_STAMP(0);
   __builtin_assume(wave >= 0 && wave < NW);
   const int wc = wave / WAVES_P, wp = wave % WAVES_P;
@@ -630,6 +640,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
         vmax = ooff[i][j] != kOOB ? fmaxf(vmax, m) : vmax;
       }
     }
+    SMPQ_STAMP(25);
   } else {
     float o[WC][WP][4];
 #pragma unroll
@@ -758,6 +769,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       // stage the [L][BP][BC] tile in the operand area (every wave is past its last fragment
       // read after this barrier), then copy it out row-major in 16-B pieces
       __syncthreads();
+      SMPQ_STAMP(26);
 #pragma unroll
       for (int i = 0; i < WC; ++i)
 #pragma unroll
@@ -765,6 +777,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 #pragma unroll
           for (int l = 0; l < L; ++l) *reinterpret_cast<unsigned*>(lds + tile_word(0, i, j, l)) = wq[i][j][l];
       __syncthreads();
+      SMPQ_STAMP(27);
       constexpr int RCPR = BC / 16, ITEMS = TILEB / 16;
 #pragma unroll
       for (int k = 0; k < (ITEMS + 64 * NW - 1) / (64 * NW); ++k) {
@@ -800,7 +813,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     unsigned id, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    smpq_stamps[((size_t)bid * NW + wave) * 32 + 23] = ((unsigned long long)(xcc & 0xf) << 16) | ((id >> 8) & 0xff);
+    stamp_base[23] = ((unsigned long long)(xcc & 0xf) << 16) | ((id >> 8) & 0xff);
   }
 #endif
 }

@@ -80,7 +80,8 @@ int run(int argc, char** argv) {
 #endif
   auto kern = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, 2, false, NST, BK, 1, false>;
   const int nsteps = a.ksteps / (BK / 64);
-  const int lds = std::min(nsteps, NST) * STAGE;
+  constexpr int TILEB = L * BP * BC;  // the staged output tile (WC % 4 == 0 and BC >= 128: lines)
+  const int lds = std::max(std::min(nsteps, NST) * STAGE, TILEB);
   CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -107,7 +108,7 @@ int run(int argc, char** argv) {
     std::sort(v.begin(), v.end());
     return v.empty() ? 0.0 : v[v.size() / 2];
   };
-  std::vector<double> pro, step, rd, iss, mf, rest, epi, life, skew;
+  std::vector<double> pro, step, rd, iss, mf, rest, epi, life, skew, wait0, kloop, e_comp, e_sync, e_stage, e_out;
   for (int b = 0; b < blocks; ++b) {
     unsigned long long bar6[NW];
     for (int w = 0; w < NW; ++w) {
@@ -121,7 +122,13 @@ int run(int argc, char** argv) {
         mf.push_back((double)(t[20] - t[19]));
         rest.push_back((double)(t[9] - t[20]));
       }
+      wait0.push_back((double)(t[2] - t[1]));
+      kloop.push_back((double)(t[21] - t[2]));
       epi.push_back((double)(t[22] - t[21]));
+      if (t[25]) e_comp.push_back((double)(t[25] - t[21]));
+      if (t[26] && t[25]) e_sync.push_back((double)(t[26] - t[25]));
+      if (t[27] && t[26]) e_stage.push_back((double)(t[27] - t[26]));
+      if (t[27]) e_out.push_back((double)(t[22] - t[27]));
       life.push_back((double)(t[22] - t[0]));
       bar6[w] = t[8];
     }
@@ -162,9 +169,12 @@ int run(int argc, char** argv) {
   printf("{\"shape\": \"%dx%d %d->%d at %d^2, B=%d, BK=%d\", \"blocks\": %d, \"ksteps\": %d, \"kernel_us\": %.1f, "
          "\"median_cycles\": {\"prologue\": %.0f, \"per_k_step\": %.0f, \"step6_barrier_to_frags\": %.0f, "
          "\"step6_dma_issue\": %.0f, \"step6_mfma_issue_to_retire\": %.0f, \"step6_to_next_barrier\": %.0f, "
-         "\"epilogue\": %.0f, \"block_life\": %.0f, \"barrier_exit_skew\": %.0f}}\n",
+         "\"epilogue\": %.0f, \"block_life\": %.0f, \"barrier_exit_skew\": %.0f, \"first_dma_wait\": %.0f, "
+         "\"k_loop_after_first_barrier\": %.0f, \"epi_loads_and_math\": %.0f, \"epi_first_sync\": %.0f, "
+         "\"epi_lds_stage\": %.0f, \"epi_copy_out_and_flag\": %.0f}}\n",
          k, k, cin, cout, hw, n, BK, blocks, nsteps, ms * 1e3, med(pro), med(step), med(rd), med(iss), med(mf),
-         med(rest), med(epi), med(life), med(skew));
+         med(rest), med(epi), med(life), med(skew), med(wait0), med(kloop), med(e_comp), med(e_sync), med(e_stage),
+         med(e_out));
   return 0;
 }
 
