@@ -16,4 +16,8 @@ SHAPES = [  # name, cin, cout, k, stride, hin, residual, wlimbs
     ("ds_512_1024_28s2", 512, 1024, 1, 2, 28, False, 3),
     ("ds_256_512_56s2", 256, 512, 1, 2, 56, False, 3),
     ("ds_64_256_56", 64, 256, 1, 1, 56, False, 3),
+    # the strided downsamples on an input already subsampled by 2 (same outputs, stride 1)
+    ("dsq_1024_2048_7s1", 1024, 2048, 1, 1, 7, False, 3),
+    ("dsq_512_1024_14s1", 512, 1024, 1, 1, 14, False, 3),
+    ("dsq_256_512_28s1", 256, 512, 1, 1, 28, False, 3),
 ]
