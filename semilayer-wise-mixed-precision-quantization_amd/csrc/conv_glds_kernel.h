@@ -75,7 +75,8 @@ __device__ unsigned long long* smpq_stamps;
 // BK: K bytes per stage and row. 64 = one MFMA K; 128 (cin % 128 == 0) = two, and every DMA piece
 // is then 8 whole 128-B lines instead of 16 half lines (half the TA/TD work per byte).
 // LEAN (0: the general epilogue; 1: lean, ReLU and residual decided at run time; 2: lean with
-// ReLU, no residual — conv1 / conv2; 3: lean with ReLU and a limb-plane residual — conv3): the
+// ReLU, no residual — conv1 / conv2; 3: lean with ReLU and a limb-plane residual — conv3; 4: lean
+// without ReLU or residual — the downsample convs): the
 // static-range epilogue that only emits the next conv's limb planes (no fp32 output, no
 // fp32 residual, no per-image maxima): the output quantizer's 1/step is folded into the column
 // scale / shift and the residual scale, ReLU and the code clamp are one v_med3, and overflow is
@@ -265,7 +266,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   constexpr int NQ = TR ? WC / 4 : 1;
   const bool lines = (kAblate & 32) ? BC >= 128 : (BC >= 128 || BC == a.cout);
   // limb-plane residual (compile-time in the LEAN 2 / 3 variants: no merged paths in the epilogue)
-  const bool has_rq = LEAN == 3 || (LEAN != 2 && a.res_q != nullptr);
+  const bool has_rq = LEAN == 3 || (LEAN != 2 && LEAN != 4 && a.res_q != nullptr);
   const bool stage_res = TR && has_rq && lines, stage_out = TR && a.yq && lines;
   unsigned qoff[NQ][WP];
 #pragma unroll
@@ -620,7 +621,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     // register pairs and cost more moves than they save here.
     const float inv = a.yq_inv;
     const float rsq = a.res_scale * inv;
-    const bool relu = LEAN >= 2 || a.relu != 0;
+    const bool relu = LEAN == 2 || LEAN == 3 || (LEAN != 4 && a.relu != 0);
     const float lo = relu ? 0.f : -qmax;
     const bool has_res = has_rq;
 #pragma unroll
@@ -915,10 +916,12 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
     auto k10 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kLean, PIPE, false>;
     auto k20 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 2 : kLean, PIPE, false>;
     auto k30 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 3 : kLean, PIPE, false>;
+    auto k40 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, L >= 2 ? 4 : 0, PIPE, false>;
     auto k01 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, 0, PIPE, LW == 1>;
     auto k11 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kLean, PIPE, LW == 1>;
     auto k21 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 2 : kLean, PIPE, LW == 1>;
     auto k31 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 3 : kLean, PIPE, LW == 1>;
+    auto k41 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, L >= 2 ? 4 : 0, PIPE, LW == 1>;
     auto set_lds = [](const void* k) {
       const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                kMaxNeed < kMaxLds ? kMaxNeed : kMaxLds);
@@ -926,15 +929,20 @@ static int launch_one(const ConvArgs& a, hipStream_t stream) {
       return e;
     };
     using KFn = decltype(k00);
-    static const KFn fns[8] = {k00, k10, k20, k30, k01, k11, k21, k31};
-    static hipError_t attrs[8];
+    static const KFn fns[10] = {k00, k10, k20, k30, k40, k01, k11, k21, k31, k41};
+    static hipError_t attrs[10];
     static const bool attrs_set = [&] {
-      for (int i = 0; i < 8; ++i) attrs[i] = set_lds(reinterpret_cast<const void*>(fns[i]));
+      for (int i = 0; i < 10; ++i) attrs[i] = set_lds(reinterpret_cast<const void*>(fns[i]));
       return true;
     }();
     (void)attrs_set;
-    const int ev = !lean ? 0 : (!kV || !a.relu) ? 1 : (a.res_q ? 3 : 2);
-    const int vi = ev + ((LW == 1 && a.has_offset) ? 4 : 0);
+    // variant: general / lean: ReLU + no residual, ReLU + limb-plane residual (one weight limb),
+    // neither ReLU nor residual (the downsample convs), anything else at run time
+    const int ev = !lean ? 0
+                   : (kV && a.relu) ? (a.res_q ? 3 : 2)
+                   : (!a.relu && !a.res_q) ? 4
+                                           : 1;
+    const int vi = ev + ((LW == 1 && a.has_offset) ? 5 : 0);
     if (attrs[vi] != hipSuccess) return check_hip(attrs[vi], "qconv_glds_kernel LDS attribute");
     hipLaunchKernelGGL(fns[vi], dim3((unsigned)(mt * nt)), dim3(64 * WAVES_C * WAVES_P), lds_bytes, stream, b);
     return check_hip(hipGetLastError(), "qconv_glds_kernel launch");
