@@ -93,3 +93,46 @@ def test_halo_refuses_what_it_does_not_run(gpu):
                      want_f32=False)
     with pytest.raises(_lib.SmpqError, match="halo"):
         ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, tile_cfg=c)
+
+
+@pytest.mark.parametrize("arch,assign", [("resnet18", "r18_u8"), ("resnet50", "r50_mixed")])
+def test_model_forward_halo_tiles_bitwise(gpu, arch, assign):
+    """A whole static-range forward with every 3x3 / stride-1 conv on a halo tile gives the same
+    logits, bit for bit, as with every conv on the implicit-GEMM tiles (and the halo kernel did
+    run: its configurations were chosen for those convs)."""
+    from smpq import engine, ops
+    from test_gpu import build_model
+    net = build_model(gpu, arch, assign, None)
+    x = torch.randn(4, 3, 224, 224, generator=torch.Generator().manual_seed(7)).to(gpu)
+    orig = ops._choose_tile
+    picked = []
+
+    def choose(kind):
+        def pick(key, run, cands):
+            halo = [c for c in cands if ops.tile_kind(c) == ops.TILE_HALO3X3]
+            gemm = [c for c in cands if ops.tile_kind(c) != ops.TILE_HALO3X3]
+            # a halo tile only where the call is one it runs (lean, ReLU): key = n|h|w|cin|cout|kh|kw|
+            # stride|pad|limbs|wlimbs|res_f32|emit_q|want_f32|res_q
+            lean = key[5] == 3 and key[7] == 1 and key[12] and not key[13] and not key[14] and not key[11]
+            if kind == "halo" and halo and lean:
+                picked.append(halo[0])
+                return halo[0]
+            return gemm[0] if gemm else None
+        return pick
+
+    outs = {}
+    try:
+        engine.USE_GRAPH[0] = False
+        for kind in ("gemm", "halo"):
+            ops._TUNED.clear()
+            ops._choose_tile = choose(kind)
+            engine.new_evaluation(net)
+            with torch.no_grad():
+                net(x)  # calibration (dynamic ranges: the general epilogue, never a halo tile)
+                outs[kind] = net(x).clone()
+    finally:
+        ops._choose_tile = orig
+        ops._TUNED.clear()
+        engine.USE_GRAPH[0] = True
+    assert picked, "no conv ran on a halo tile"
+    assert torch.equal(outs["halo"], outs["gemm"])
