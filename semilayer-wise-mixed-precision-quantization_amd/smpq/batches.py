@@ -54,10 +54,13 @@ class DeviceBatches:
         it = iter(self.loader)
         nxt = [None]
 
+        from .engine import CAPTURE_LOCK
+
         def fetch():
             try:
-                x, y = next(it)
-                with torch.cuda.device(self.dev):
+                x, y = next(it)  # the loader's own work (host only) runs beside anything
+                # device work waits for a graph capture on the main thread to end (engine.CAPTURE_LOCK)
+                with CAPTURE_LOCK, torch.cuda.device(self.dev):
                     nxt[0] = self._stage(x, y)
             except StopIteration:
                 nxt[0] = StopIteration

@@ -41,6 +41,8 @@ content fingerprints of the conv weights / metadata / BN tensors (smpq/fingerpri
 after every forward: a write through ``.data`` (no version bump) is detected, the result is
 discarded and recomputed from freshly packed weights.
 """
+import threading
+
 import torch
 import torch.nn.functional as F
 
@@ -67,6 +69,8 @@ FUSED_STEM = [_os.environ.get("SMPQ_FUSED_STEM", "1") != "0"]
 CONCURRENT_DS = [_os.environ.get("SMPQ_CONCURRENT_DS", "1") != "0"]
 # static range: the batch split into this many slices, each on its own stream (concurrent kernels)
 STREAMS = [int(_os.environ.get("SMPQ_STREAMS", "2"))]
+# static range, batch slices: enqueue (and capture) the slices' launches interleaved
+INTERLEAVE = [_os.environ.get("SMPQ_INTERLEAVE", "1") != "0"]
 stats.setdefault("graph_captures", 0)
 stats.setdefault("graph_replays", 0)
 
@@ -241,7 +245,7 @@ def _side_stream(device, lane):
     return _stream((device, "ds", lane))
 
 
-def block_forward(blk, x, ctx=None, last=False):
+def _block_gen(blk, x, ctx=None, last=False):
     """One BasicBlock / Bottleneck on an Act; returns the output Act. In static mode no
     activation is stored in fp32 except the downsample's identity and the last block's output
     (avgpool): the identity of a block without downsample is read from its input's limb planes.
@@ -279,9 +283,13 @@ def block_forward(blk, x, ctx=None, last=False):
         if side is not None:
             torch.cuda.current_stream().wait_stream(side)
 
+    if blk.downsample is not None:
+        yield
     t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
+    yield
     if hasattr(blk, "conv3"):  # Bottleneck (resnet.py:97-116)
         t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
+        yield
         join()
         return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax,
                         want_f32=last)
@@ -289,6 +297,20 @@ def block_forward(blk, x, ctx=None, last=False):
     join()
     return run_conv(blk.conv2, blk.bn2, t1, True, residual=identity, ctx=ctx, want_amax=out_amax,
                     want_f32=last)
+
+
+def block_forward(blk, x, ctx=None, last=False):
+    """One block, enqueued in one go (_block_gen run to completion); returns the output Act."""
+    return _drain(_block_gen(blk, x, ctx, last))
+
+
+def _drain(gen):
+    """Run a launch generator (_block_gen / _slice_gen) to completion; returns its value."""
+    while True:
+        try:
+            next(gen)
+        except StopIteration as e:
+            return e.value
 
 
 def stem_s2d_plan(conv, bn):
@@ -380,12 +402,23 @@ def _head(model, feat):
     return model.fc(feat.mean(dim=(1, 2)))
 
 
-def _features(model, x, ctx):
+def _features_gen(model, x, ctx):
+    """The stem and every block, yielding after each launch step (see _forward's slices)."""
     act = stem_forward(model, x, ctx)
+    yield
     blocks = _blocks(model)
     for i, blk in enumerate(blocks):
-        act = block_forward(blk, act, ctx, last=(i == len(blocks) - 1))
+        act = yield from _block_gen(blk, act, ctx, last=(i == len(blocks) - 1))
     return act.f32
+
+
+def _features(model, x, ctx):
+    return _drain(_features_gen(model, x, ctx))
+
+
+def _slice_gen(model, x, ctx):
+    feat = yield from _features_gen(model, x, ctx)
+    return _head(model, feat)
 
 
 def _forward(model, x, ctx):
@@ -407,14 +440,30 @@ def _forward(model, x, ctx):
             for m in model.modules():
                 if id(m) in ctx.ranges:
                     ctx.range_tensor(m)
-        logits = []
         lanes = min(nst, len(parts))
+        logits = [None] * len(parts)
         for i in range(lanes):
             _stream((x.device, "slice", i)).wait_stream(main)
-        for i, (s0, s1) in enumerate(parts):
-            with torch.cuda.stream(_stream((x.device, "slice", i % lanes))):
-                ctx.n, ctx.lane = s1 - s0, i % lanes
-                logits.append(_head(model, _features(model, x[s0:s1], ctx)))
+        # The slices' launches are enqueued interleaved, one launch step of each slice in turn
+        # (INTERLEAVE; otherwise slice after slice). A replayed HIP graph dispatches its kernel
+        # nodes in capture order, so with slice-after-slice capture the second slice's chain only
+        # starts once the host has dispatched the whole first chain.
+        for g0 in range(0, len(parts), lanes):
+            gens = {i: _slice_gen(model, x[parts[i][0]:parts[i][1]], ctx)
+                    for i in range(g0, min(len(parts), g0 + lanes))}
+            while gens:
+                for i in list(gens):
+                    with torch.cuda.stream(_stream((x.device, "slice", i % lanes))):
+                        ctx.n, ctx.lane = parts[i][1] - parts[i][0], i % lanes
+                        try:
+                            if INTERLEAVE[0]:
+                                next(gens[i])
+                            else:
+                                logits[i] = _drain(gens[i])
+                                del gens[i]
+                        except StopIteration as e:
+                            logits[i] = e.value
+                            del gens[i]
         for i in range(lanes):
             main.wait_stream(_stream((x.device, "slice", i)))
         ctx.n, ctx.lane = n, None
@@ -584,7 +633,7 @@ def _graph_base(cal):
     """What every captured graph of a model depends on besides its input's shape and address:
     the calibration (ranges, signature) and the forward's structure knobs."""
     return (cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0], CONCURRENT_DS[0], STREAMS[0],
-            ops.KMAJOR[0])
+            ops.KMAJOR[0], INTERLEAVE[0])
 
 
 def _graph_key(model, x, cal):
@@ -621,7 +670,20 @@ def _graph_ready(model, x, cal):
 GRAPHS_PER_MODEL = [int(_os.environ.get("SMPQ_GRAPHS", "4"))]
 
 
+# Held while a HIP graph is being captured. torch captures in the default "global" mode, in which
+# device allocations and synchronising calls made by ANY thread during the capture are errors (or
+# end up in the graph); smpq.batches' staging worker takes this lock around its device work
+# (pinned-buffer waits, the side-stream copies and their allocations), so a batch staged while
+# the evaluation loop captures waits for the capture to end instead of breaking it.
+CAPTURE_LOCK = threading.Lock()
+
+
 def _capture(model, x_in, cal):
+    with CAPTURE_LOCK:
+        return _capture_locked(model, x_in, cal)
+
+
+def _capture_locked(model, x_in, cal):
     g = torch.cuda.CUDAGraph()
     ctx = Ctx(x_in.shape[0], x_in.device, ranges=cal[0], cache=cal[2])
     # one memory pool for all of the model's graphs: they are replayed one at a time on one stream

@@ -216,11 +216,31 @@ def stem_conv_s2d(xq, x_absmax, codes, h, w, col_scale, col_shift, relu=True, y_
     wlimbs, cout, K = codes.shape
     _req(K == 256, "stem_conv_s2d: codes must come from pack_weights_s2d")
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    if emit_range is None:
+        want_f32 = True
     y = torch.empty(n, ho, wo, cout, dtype=torch.float32, device=xq.device) if want_f32 else None
     yq = None
     if emit_range is not None:
         _req(overflow is not None, "stem_conv_s2d: emit_range needs an overflow flag tensor")
         yq = torch.empty(limbs, n, ho, wo, cout, dtype=torch.int8, device=xq.device)
+    per_img = max(limbs * h2 * w2 * 16, (4 if want_f32 else 0) * ho * wo * cout,
+                  (limbs if yq is not None else 0) * ho * wo * cout)
+    nchunk = PLANE_LIMIT // per_img
+    _req(nchunk >= 1, "stem_conv_s2d: one image's planes exceed 2 GiB")
+    if n > nchunk:
+        # 32-bit plane offsets in the kernel: the images in chunks, as conv2d_q does (every image
+        # is independent, so the result is that of one launch)
+        for i0 in range(0, n, nchunk):
+            i1 = min(n, i0 + nchunk)
+            r = stem_conv_s2d(xq[:, i0:i1].contiguous(), x_absmax[i0:i1], codes, h, w, col_scale, col_shift, relu,
+                              None if y_absmax is None else y_absmax[i0:i1], tile_cfg, emit_range, overflow, want_f32)
+            if emit_range is None:
+                y[i0:i1].copy_(r)
+            else:
+                if y is not None:
+                    y[i0:i1].copy_(r[0])
+                yq[:, i0:i1].copy_(r[1])
+        return y if emit_range is None else (y, yq)
     lib = _lib.load()
     hook = _CONV_HOOK[0]
     if hook is not None:
@@ -444,7 +464,6 @@ def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_sh
         # image is independent, so the result is the same as one launch)
         for i0 in range(0, n, nchunk):
             i1 = min(n, i0 + nchunk)
-            yq_c = None if yq is None else torch.empty(limbs, i1 - i0, ho, wo, cout, dtype=torch.int8, device=xq.device)
             r = conv2d_q(xq[:, i0:i1].contiguous(), x_absmax[i0:i1], codes, offset, kh, kw, stride, pad,
                          col_scale, col_shift, residual=None if residual is None else residual[i0:i1], relu=relu,
                          y_absmax=None if y_absmax is None else y_absmax[i0:i1],
@@ -529,16 +548,18 @@ def tile_table_info():
             "autotuned": _TABLE["tuned"]}
 
 
-def _choose_tile(key, run, cands):
-    """The tile for ``key``: cached, from the table, or autotuned (None: the C-ABI default)."""
-    cfg = _TUNED.get(key)
+def _choose_tile(key, run, cands, variant=None):
+    """The tile for ``key``: cached, from the table, or autotuned (None: the C-ABI default).
+    ``variant`` separates calls of one key whose candidate sets differ (the cache only)."""
+    ckey = key if variant is None else (key, variant)
+    cfg = _TUNED.get(ckey)
     if cfg is not None:
         return cfg
     if not _TABLE.get("loaded"):
         load_tile_table()
     t = _TABLE["entries"].get(key_str(key))
     if t is not None and t in cands:
-        _TUNED[key] = t
+        _TUNED[ckey] = t
         _TABLE["hits"] += 1
         return t
     if not AUTOTUNE[0] or torch.cuda.is_current_stream_capturing():
@@ -566,7 +587,7 @@ def _choose_tile(key, run, cands):
             best = (t_med, c)
     if best is None:
         return None
-    _TUNED[key] = best[1]
+    _TUNED[ckey] = best[1]
     _TABLE["tuned"] += 1
     return best[1]
 
@@ -596,7 +617,13 @@ def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, 
                  residual=residual, relu=relu, y_absmax=y_absmax, out=out, tile_cfg=c,
                  emit_range=emit_range, overflow=overflow, want_f32=want_f32,
                  residual_q=residual_q, residual_range=residual_range)
-    cfg = _choose_tile(key, run, [c for c in tile_configs() if _tile_fits(c, limbs, wlimbs, cout, cin, kh)])
+    # the halo tiles run only the static-range limb-plane epilogue with ReLU (stride 1 / pad 1 for
+    # now): the key does not carry relu / y_absmax, so other calls of a key never see them
+    halo_ok = bool(relu and emit_range is not None and not want_f32 and residual is None and residual_q is None
+                   and y_absmax is None and out is None and kh == 3 and kw == 3 and stride == 1 and pad == 1)
+    cands = [c for c in tile_configs() if _tile_fits(c, limbs, wlimbs, cout, cin, kh)
+             and (halo_ok or tile_kind(c) != TILE_HALO3X3)]
+    cfg = _choose_tile(key, run, cands, variant=None if halo_ok else "nohalo")
     return conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_shift,
                     residual=residual, relu=relu, y_absmax=y_absmax, out=out,
                     tile_cfg=-1 if cfg is None else cfg, emit_range=emit_range, overflow=overflow,

@@ -16,7 +16,16 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 CASES = [("resnet18", "r18_u8"), ("resnet50", "r50_mixed")]
+MODES = ("static", "dynamic")
 GLOBAL_BATCH, STEPS, BATCHES = 8, 6, 3  # step 0 calibrates, 1-3 capture a graph per batch, 4-5 replay
+# SMPQ_DPW_CFG (json) overrides these: the full per-rank size of BASELINE configs[3] is
+# {"global_batch": 512, "steps": 7, "batches": 4, "cases": [["resnet50", "r50_mixed"]], "modes": ["static"]}
+if os.environ.get("SMPQ_DPW_CFG"):
+    import json
+    _c = json.loads(os.environ["SMPQ_DPW_CFG"])
+    GLOBAL_BATCH, STEPS, BATCHES = _c["global_batch"], _c["steps"], _c["batches"]
+    CASES = [tuple(c) for c in _c["cases"]]
+    MODES = tuple(_c["modes"])
 
 
 def global_batches(dev):
@@ -46,19 +55,24 @@ def main():
         s, e = dp.shard_range(GLOBAL_BATCH, rank, world)
         shards = [x[s:e].contiguous() for x in global_batches(dev)]  # this rank's, resident
         for arch, assign in CASES:
-            for mode in ("static", "dynamic"):
+            for mode in MODES:
                 engine.set_range_mode(mode)
                 net = model(arch, assign, dev)
                 outs = []
                 r0 = stats["graph_replays"]
                 with torch.no_grad(), dp.lockstep():
                     for step in range(STEPS):
+                        if step == 1:
+                            c1 = stats["calibrations"]
                         y = net(shards[step % BATCHES])
                         outs.append(dp.gather_logits(y, world).cpu())
                 if mode == "static":
                     assert stats["graph_replays"] > r0, "the static forward never replayed a graph"
+                info = {"recalibrations_after_first": stats["calibrations"] - c1,
+                        "graph_replays": stats["graph_replays"] - r0, "rows_per_rank": e - s}
                 if rank == 0:
                     torch.save(outs, os.path.join(outdir, "%s_%s.pt" % (arch, mode)))
+                    torch.save(info, os.path.join(outdir, "%s_%s_info.pt" % (arch, mode)))
         engine.set_range_mode("static")
     finally:
         dist.destroy_process_group()

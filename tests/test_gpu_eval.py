@@ -132,3 +132,33 @@ def test_repeated_evaluations_keep_graphs_and_host_batches_match(gpu):
     r0 = stats["repack"]
     assert same(functions.evaluate_acc_loss_softmax(net, gpu, on_dev), ref)
     assert stats["repack"] > r0
+
+
+def test_host_batches_staged_during_graph_capture(gpu):
+    """DeviceBatches stages batch i+1 on a worker thread while batch i runs, and a
+    forward on a new input address captures a HIP graph. A loader that is slow in __next__ makes the
+    worker's device work (pinned copy, side-stream allocation and copy, event) fall inside the
+    capture window; engine.CAPTURE_LOCK makes it wait for the capture. Results equal the
+    device-resident loader's bit for bit, and graphs were captured meanwhile."""
+    import time
+
+    import functions
+    from smpq import stats
+    from test_gpu import build_model
+    net = build_model(gpu, "resnet18", "r18_u8")
+    g = torch.Generator().manual_seed(13)
+    host = [(torch.randn(6, 3, 224, 224, generator=g), torch.randint(0, 1000, (6,), generator=g)) for _ in range(6)]
+    on_dev = [(x.to(gpu), y.to(gpu)) for x, y in host]
+
+    class Slow:
+        def __iter__(self):
+            for i, b in enumerate(host):
+                if i:
+                    time.sleep(0.02 * i)  # staggered: some stagings land inside a capture
+                yield b
+    c0 = stats["graph_captures"]
+    runs = [functions.evaluate_acc_loss_softmax(net, gpu, Slow()) for _ in range(2)]
+    assert stats["graph_captures"] > c0  # the first slow evaluation captured its graphs
+    ref = functions.evaluate_acc_loss_softmax(net, gpu, on_dev)
+    for r in runs:
+        assert r[0] == ref[0] and r[1] == ref[1] and all(torch.equal(a, b) for a, b in zip(r[2], ref[2]))
