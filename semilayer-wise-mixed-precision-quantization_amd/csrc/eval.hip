@@ -136,48 +136,76 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const float* __restrict__ 
                                                      __fdiv_rn(s.w, d));
 }
 
-// logits[i][o] = fc_b[o] + sum_k pooled[i][k] * w[o][k], the sum as one fmaf chain over k = 0..c-1
-// (then + bias): the order depends on nothing but c, so a row's logits are the same bits in any
-// batch. Block tile: 16 images x 64 outputs, K chunks of 64 staged in LDS (k-major); thread
-// (i = t / 16, o4 = t % 16) owns outputs 4 o4 .. 4 o4 + 3 of image i.
-constexpr int kFcI = 16, kFcO = 64, kFcK = 64;
-__global__ __launch_bounds__(256) void fc_kernel(const float* __restrict__ pooled, int n, int c,
+// logits[i][o] = fc_b[o] + ((s_0 + s_1) + s_2) + s_3, where s_q = sum over the q-th quarter of k
+// (kFcQ-aligned ranges fixed by c alone) as one fmaf chain in k order: the order depends on nothing
+// but c, so a row's logits are the same bits in any batch. Block: 8 images x 64 outputs; its 512
+// threads are 4 K-quarter groups of 128 (group g = threads 128 g ..), thread (i = t / 16, o4 = t % 16)
+// of a group owns outputs 4 o4 .. 4 o4 + 3 of image i over the group's quarter. Each group stages
+// its own 64-k chunks in LDS (k-major), the next chunk's global loads in flight under the current
+// chunk's FMAs; the groups' partials meet in LDS and group 0 adds them in quarter order.
+// (Round 4's one-chain kernel ran 16 x 64 tiles over all of k per thread: 110-190 us per R50 slice
+// of 128 images, a fifth of the chip busy; this one splits the chain four ways over 4x the blocks.)
+constexpr int kFcI = 8, kFcO = 64, kFcK = 64, kFcG = 4;
+__global__ __launch_bounds__(512) void fc_kernel(const float* __restrict__ pooled, int n, int c,
                                                  const float* __restrict__ w, const float* __restrict__ b, int nout,
                                                  float* __restrict__ logits) {
-  // k-major LDS images (rows padded to keep the transposing writes at <= 4-way bank conflicts)
-  __shared__ __attribute__((aligned(16))) float sp[kFcK][kFcI + 4];
-  __shared__ __attribute__((aligned(16))) float sw[kFcK][kFcO + 4];
-  const int tid = threadIdx.x;
+  // per group, k-major LDS images (rows padded: the transposing writes stay at <= 4-way conflicts)
+  __shared__ __attribute__((aligned(16))) float sp[kFcG][kFcK][kFcI + 4];
+  __shared__ __attribute__((aligned(16))) float sw[kFcG][kFcK][kFcO + 4];
+  __shared__ __attribute__((aligned(16))) float part[kFcG - 1][kFcI][kFcO];
+  const int grp = threadIdx.x >> 7, tid = threadIdx.x & 127;
   const int i0 = blockIdx.y * kFcI, o0 = blockIdx.x * kFcO;
   const int ti = tid / 16, to = tid % 16;
+  // quarter ranges: whole 64-k chunks, fixed by c
+  const int cq = ((c + kFcG - 1) / kFcG + kFcK - 1) / kFcK * kFcK;
+  const int kb = min(c, grp * cq), ke = min(c, kb + cq);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < c; k0 += kFcK) {
-    // 16-B loads along k (16 lanes = one 256-B row piece): pooled 16 images x 64 k (one per
-    // thread), weights 64 outputs x 64 k (four per thread)
+  // staging: pooled 8 images x 64 k (one float4 per thread of the group); weights 64 x 64 k
+  // (eight float4 per thread)
+  float4 vp, vw[8];
+  auto load = [&](int k0) {
     {
       const int ii = tid / 16, kq = tid % 16, img = i0 + ii, k = k0 + 4 * kq;
-      const float4 v = (img < n && k < c) ? *reinterpret_cast<const float4*>(pooled + (long long)img * c + k)
-                                          : make_float4(0.f, 0.f, 0.f, 0.f);
-      sp[4 * kq][ii] = v.x;
-      sp[4 * kq + 1][ii] = v.y;
-      sp[4 * kq + 2][ii] = v.z;
-      sp[4 * kq + 3][ii] = v.w;
+      vp = (tid < 128 && img < n && k < ke) ? *reinterpret_cast<const float4*>(pooled + (long long)img * c + k)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = tid + 256 * r, oo = e / 16, kq = e % 16, o = o0 + oo, k = k0 + 4 * kq;
-      const float4 v = (o < nout && k < c) ? *reinterpret_cast<const float4*>(w + (long long)o * c + k)
-                                           : make_float4(0.f, 0.f, 0.f, 0.f);
-      sw[4 * kq][oo] = v.x;
-      sw[4 * kq + 1][oo] = v.y;
-      sw[4 * kq + 2][oo] = v.z;
-      sw[4 * kq + 3][oo] = v.w;
+    for (int r = 0; r < 8; ++r) {
+      const int e = tid + 128 * r, oo = e / 16, kq = e % 16, o = o0 + oo, k = k0 + 4 * kq;
+      vw[r] = (o < nout && k < ke) ? *reinterpret_cast<const float4*>(w + (long long)o * c + k)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+  };
+  auto store = [&]() {
+    {
+      const int ii = tid / 16, kq = tid % 16;
+      sp[grp][4 * kq][ii] = vp.x;
+      sp[grp][4 * kq + 1][ii] = vp.y;
+      sp[grp][4 * kq + 2][ii] = vp.z;
+      sp[grp][4 * kq + 3][ii] = vp.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int e = tid + 128 * r, oo = e / 16, kq = e % 16;
+      sw[grp][4 * kq][oo] = vw[r].x;
+      sw[grp][4 * kq + 1][oo] = vw[r].y;
+      sw[grp][4 * kq + 2][oo] = vw[r].z;
+      sw[grp][4 * kq + 3][oo] = vw[r].w;
+    }
+  };
+  // every group runs the same number of chunk steps (barriers are block-wide); a group past its
+  // range computes nothing
+  const int steps = (cq + kFcK - 1) / kFcK;
+  load(kb);
+  for (int s = 0; s < steps; ++s) {
+    const int k0 = kb + s * kFcK;
+    store();
     __syncthreads();
-    const int kn = min(kFcK, c - k0);
+    if (s + 1 < steps) load(k0 + kFcK);  // in flight under this chunk's FMAs
+    const int kn = max(0, min(kFcK, ke - k0));
     for (int kk = 0; kk < kn; ++kk) {
-      const float pv = sp[kk][ti];
-      const float4 wv = *reinterpret_cast<const float4*>(&sw[kk][4 * to]);
+      const float pv = sp[grp][kk][ti];
+      const float4 wv = *reinterpret_cast<const float4*>(&sw[grp][kk][4 * to]);
       acc[0] = __fmaf_rn(pv, wv.x, acc[0]);
       acc[1] = __fmaf_rn(pv, wv.y, acc[1]);
       acc[2] = __fmaf_rn(pv, wv.z, acc[2]);
@@ -185,12 +213,21 @@ __global__ __launch_bounds__(256) void fc_kernel(const float* __restrict__ poole
     }
     __syncthreads();
   }
+  if (grp > 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) part[grp - 1][ti][4 * to + j] = acc[j];
+  }
+  __syncthreads();
+  if (grp > 0) return;
   const int img = i0 + ti;
   if (img >= n) return;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int o = o0 + 4 * to + j;
-    if (o < nout) logits[(long long)img * nout + o] = b ? __fadd_rn(acc[j], b[o]) : acc[j];
+    float v = acc[j];
+#pragma unroll
+    for (int q = 0; q < kFcG - 1; ++q) v = __fadd_rn(v, part[q][ti][4 * to + j]);
+    if (o < nout) logits[(long long)img * nout + o] = b ? __fadd_rn(v, b[o]) : v;
   }
 }
 
@@ -243,7 +280,7 @@ extern "C" int smpq_avgpool_fc(const float* x, int n, int hw, int c, const float
                      pooled_ws);
   int rc = check_hip(hipGetLastError(), "avgpool_kernel launch");
   if (rc) return rc;
-  hipLaunchKernelGGL(fc_kernel, dim3((nout + kFcO - 1) / kFcO, (n + kFcI - 1) / kFcI), dim3(256), 0, stream,
+  hipLaunchKernelGGL(fc_kernel, dim3((nout + kFcO - 1) / kFcO, (n + kFcI - 1) / kFcI), dim3(512), 0, stream,
                      pooled_ws, n, c, fc_w, fc_b, nout, logits);
   return check_hip(hipGetLastError(), "fc_kernel launch");
 }

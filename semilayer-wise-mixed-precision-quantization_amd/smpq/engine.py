@@ -69,8 +69,6 @@ FUSED_STEM = [_os.environ.get("SMPQ_FUSED_STEM", "1") != "0"]
 CONCURRENT_DS = [_os.environ.get("SMPQ_CONCURRENT_DS", "1") != "0"]
 # static range: the batch split into this many slices, each on its own stream (concurrent kernels)
 STREAMS = [int(_os.environ.get("SMPQ_STREAMS", "2"))]
-# static range, batch slices: enqueue (and capture) the slices' launches interleaved
-INTERLEAVE = [_os.environ.get("SMPQ_INTERLEAVE", "1") != "0"]
 stats.setdefault("graph_captures", 0)
 stats.setdefault("graph_replays", 0)
 
@@ -232,11 +230,16 @@ def run_conv(conv, bn, act, relu, residual=None, want_amax=True, ctx=None, want_
 _STREAMS = {}
 
 
+# diagnostics: the first batch slice's stream at high priority (the others at normal priority)
+SLICE_PRIORITY = [_os.environ.get("SMPQ_SLICE_PRIORITY", "0") != "0"]
+
+
 def _stream(key):
     """A side stream per key (created once; reused by every forward and graph capture)."""
     s = _STREAMS.get(key)
     if s is None:
-        s = _STREAMS[key] = torch.cuda.Stream(device=key[0])
+        prio = -1 if (SLICE_PRIORITY[0] and key[1] == "slice" and key[2] == 0) else 0
+        s = _STREAMS[key] = torch.cuda.Stream(device=key[0], priority=prio)
     return s
 
 
@@ -245,7 +248,7 @@ def _side_stream(device, lane):
     return _stream((device, "ds", lane))
 
 
-def _block_gen(blk, x, ctx=None, last=False):
+def block_forward(blk, x, ctx=None, last=False):
     """One BasicBlock / Bottleneck on an Act; returns the output Act. In static mode no
     activation is stored in fp32 except the downsample's identity and the last block's output
     (avgpool): the identity of a block without downsample is read from its input's limb planes.
@@ -283,13 +286,9 @@ def _block_gen(blk, x, ctx=None, last=False):
         if side is not None:
             torch.cuda.current_stream().wait_stream(side)
 
-    if blk.downsample is not None:
-        yield
     t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
-    yield
     if hasattr(blk, "conv3"):  # Bottleneck (resnet.py:97-116)
         t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
-        yield
         join()
         return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax,
                         want_f32=last)
@@ -297,20 +296,6 @@ def _block_gen(blk, x, ctx=None, last=False):
     join()
     return run_conv(blk.conv2, blk.bn2, t1, True, residual=identity, ctx=ctx, want_amax=out_amax,
                     want_f32=last)
-
-
-def block_forward(blk, x, ctx=None, last=False):
-    """One block, enqueued in one go (_block_gen run to completion); returns the output Act."""
-    return _drain(_block_gen(blk, x, ctx, last))
-
-
-def _drain(gen):
-    """Run a launch generator (_block_gen / _slice_gen) to completion; returns its value."""
-    while True:
-        try:
-            next(gen)
-        except StopIteration as e:
-            return e.value
 
 
 def stem_s2d_plan(conv, bn):
@@ -402,23 +387,12 @@ def _head(model, feat):
     return model.fc(feat.mean(dim=(1, 2)))
 
 
-def _features_gen(model, x, ctx):
-    """The stem and every block, yielding after each launch step (see _forward's slices)."""
+def _features(model, x, ctx):
     act = stem_forward(model, x, ctx)
-    yield
     blocks = _blocks(model)
     for i, blk in enumerate(blocks):
-        act = yield from _block_gen(blk, act, ctx, last=(i == len(blocks) - 1))
+        act = block_forward(blk, act, ctx, last=(i == len(blocks) - 1))
     return act.f32
-
-
-def _features(model, x, ctx):
-    return _drain(_features_gen(model, x, ctx))
-
-
-def _slice_gen(model, x, ctx):
-    feat = yield from _features_gen(model, x, ctx)
-    return _head(model, feat)
 
 
 def _forward(model, x, ctx):
@@ -440,30 +414,14 @@ def _forward(model, x, ctx):
             for m in model.modules():
                 if id(m) in ctx.ranges:
                     ctx.range_tensor(m)
+        logits = []
         lanes = min(nst, len(parts))
-        logits = [None] * len(parts)
         for i in range(lanes):
             _stream((x.device, "slice", i)).wait_stream(main)
-        # The slices' launches are enqueued interleaved, one launch step of each slice in turn
-        # (INTERLEAVE; otherwise slice after slice). A replayed HIP graph dispatches its kernel
-        # nodes in capture order, so with slice-after-slice capture the second slice's chain only
-        # starts once the host has dispatched the whole first chain.
-        for g0 in range(0, len(parts), lanes):
-            gens = {i: _slice_gen(model, x[parts[i][0]:parts[i][1]], ctx)
-                    for i in range(g0, min(len(parts), g0 + lanes))}
-            while gens:
-                for i in list(gens):
-                    with torch.cuda.stream(_stream((x.device, "slice", i % lanes))):
-                        ctx.n, ctx.lane = parts[i][1] - parts[i][0], i % lanes
-                        try:
-                            if INTERLEAVE[0]:
-                                next(gens[i])
-                            else:
-                                logits[i] = _drain(gens[i])
-                                del gens[i]
-                        except StopIteration as e:
-                            logits[i] = e.value
-                            del gens[i]
+        for i, (s0, s1) in enumerate(parts):
+            with torch.cuda.stream(_stream((x.device, "slice", i % lanes))):
+                ctx.n, ctx.lane = s1 - s0, i % lanes
+                logits.append(_head(model, _features(model, x[s0:s1], ctx)))
         for i in range(lanes):
             main.wait_stream(_stream((x.device, "slice", i)))
         ctx.n, ctx.lane = n, None
@@ -633,7 +591,7 @@ def _graph_base(cal):
     """What every captured graph of a model depends on besides its input's shape and address:
     the calibration (ranges, signature) and the forward's structure knobs."""
     return (cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0], CONCURRENT_DS[0], STREAMS[0],
-            ops.KMAJOR[0], INTERLEAVE[0])
+            ops.KMAJOR[0])
 
 
 def _graph_key(model, x, cal):

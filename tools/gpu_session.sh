@@ -9,7 +9,7 @@
 #   bench      default bench line + layer table    r18 / r34  the other bench configs
 #   trace      rocprofv3 kernel trace of the default bench (+ summary, graph-region timeline)
 #   traffic    PMC FETCH/WRITE passes (tools/pmc_traffic.sh)   parity  full-size parity tests
-#   pmc        PMC screen of the hot conv kernels (tools/pmc_hot.sh)
+#   pmc        PMC screen of every conv launch + per-group summary (tools/pmc_layers.sh)
 # Any other argument (it must contain a space) is run as a command with a 600 s limit.
 # The session stops at the first failing step (no GPU work after a fault, abort or time-out).
 set -u
@@ -47,7 +47,7 @@ for step in "$@"; do
       ;;
     traffic) run 600 $o.log bash tools/pmc_traffic.sh r50_mixed 3 256 ;;
     parity) run 600 $o.log $PYT tests/test_gpu.py -m gpu -s -k full_size ;;
-    pmc) run 900 $o.log bash tools/pmc_hot.sh gpurun_out/${tag}_pmc ;;
+    pmc) run 900 $o.log bash tools/pmc_layers.sh gpurun_out/${tag}_pmc ;;
     *" "*) run 600 gpurun_out/${tag}_cmd$((++ncmd)).log bash -c "$step" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

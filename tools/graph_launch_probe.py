@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Host cost of replaying the captured R50 forward graph, and the step time, for stream-slice layouts.
+"""Host cost of replaying the captured R50 forward graph, and the step time, for several batch-slice counts.
 
-For each (slices, interleave) setting: the host wall time of CUDAGraph.replay() itself (the call
+For each slice count: the host wall time of CUDAGraph.replay() itself (the call
 returns once every node is enqueued) and the GPU step time (replay + sync) over a few replays.
 A second slice can only start once its first node has been enqueued, so a replay() that takes
 milliseconds on the host delays the second slice by about the first slice's share of it.
@@ -24,7 +24,7 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--settings", default="1:1,2:0,2:1,3:1,4:1")
+    ap.add_argument("--settings", default="1,2,3,4")
     args = ap.parse_args()
     import __graft_entry__
     __graft_entry__.build()
@@ -39,8 +39,8 @@ def main():
     with torch.no_grad():
         net(x)  # calibrate
         for st in args.settings.split(","):
-            nst, il = (int(v) for v in st.split(":"))
-            engine.STREAMS[0], engine.INTERLEAVE[0] = nst, bool(il)
+            nst = int(st)
+            engine.STREAMS[0] = nst
             for _ in range(3):
                 net(x)  # eager + capture for this layout
             per = net._smpq_graphs
@@ -57,8 +57,8 @@ def main():
                 step.append((t2 - t0) * 1e3)
             host.sort()
             step.sort()
-            r = {"slices": nst, "interleave": il, "replay_host_ms": round(host[len(host) // 2], 3),
-                 "step_ms": round(step[len(step) // 2], 3), "nodes": None}
+            r = {"slices": nst, "replay_host_ms": round(host[len(host) // 2], 3),
+                 "step_ms": round(step[len(step) // 2], 3)}
             out.append(r)
             print(json.dumps(r), flush=True)
     return out

@@ -34,6 +34,7 @@ try:
     layers = [l[:33] + l[33:43] for l in log[i + 1:i + 1 + N]]
 except StopIteration:
     layers = [""] * N
+groups = {}
 print("%-43s %5s %7s %6s %6s %6s %6s %5s %5s %5s %5s %6s" % (
     "launch (t_us)", "vgpr", "waves", "VALU/w", "SALU/w", "LDS/w", "MFMAc/w", "V/MF", "wait", "istl", "actv", "mfma%"))
 for j in range(N):
@@ -50,3 +51,22 @@ for j in range(N):
         m(a, "SQ_INSTS_LDS") / w, mf / w, m(a, "SQ_INSTS_VALU") / max(mf / 16, 1),
         m(b, "SQ_WAIT_ANY") / wc, m(b, "SQ_WAIT_INST_ANY") / wc, m(b, "SQ_ACTIVE_INST_ANY") / wc,
         100 * mf / max(gui * 128, 1)))
+    # per conv group: time-weighted MFMA busy, VALU and SALU per MFMA, wave-state shares
+    lab = layers[j] if j < len(layers) else ""
+    mm = re.match(r"\s*(\d+)->\s*(\d+) k(\d)\s+(\d+)->\s*(\d+)\s+\S+\s+([\d.]+)", lab)
+    if not mm:
+        continue
+    k, h, ho, t = int(mm.group(3)), int(mm.group(4)), int(mm.group(5)), float(mm.group(6))
+    g = ("stem+pool" if k == 7 else "3x3 stride 2" if (k == 3 and ho < h) else "3x3 %d^2" % ho if k == 3
+         else "downsample 1x1/s2" if ho < h else "1x1 %d^2" % ho)
+    acc = groups.setdefault(g, [0.0] * 7)
+    nmf = max(mf / 16, 1)
+    for q, v in enumerate((t, t * mf / max(gui * 128, 1), t * m(a, "SQ_INSTS_VALU") / nmf,
+                           t * m(a, "SQ_INSTS_SALU") / nmf, t * m(b, "SQ_WAIT_ANY") / wc,
+                           t * m(b, "SQ_WAIT_INST_ANY") / wc, 1.0)):
+        acc[q] += v
+print()
+print("%-20s %9s %8s %9s %9s %8s %8s %4s" % ("group", "t_us", "mfma%", "VALU/MF", "SALU/MF", "wait%", "istall%", "n"))
+for g, (t, mfp, va, sa, wt, ist, n) in sorted(groups.items(), key=lambda kv: -kv[1][0]):
+    print("%-20s %9.1f %8.1f %9.2f %9.2f %8.1f %8.1f %4d" % (g, t, 100 * mfp / t, va / t, sa / t, 100 * wt / t,
+                                                           100 * ist / t, n))
