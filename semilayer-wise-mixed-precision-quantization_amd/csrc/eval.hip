@@ -137,15 +137,16 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const float* __restrict__ 
 }
 
 // logits[i][o] = fc_b[o] + ((s_0 + s_1) + s_2) + s_3, where s_q = sum over the q-th quarter of k
-// (kFcQ-aligned ranges fixed by c alone) as one fmaf chain in k order: the order depends on nothing
+// (kFcK-aligned ranges fixed by c alone) as one fmaf chain in k order: the order depends on nothing
 // but c, so a row's logits are the same bits in any batch. Block: 8 images x 64 outputs; its 512
 // threads are 4 K-quarter groups of 128 (group g = threads 128 g ..), thread (i = t / 16, o4 = t % 16)
 // of a group owns outputs 4 o4 .. 4 o4 + 3 of image i over the group's quarter. Each group stages
-// its own 64-k chunks in LDS (k-major), the next chunk's global loads in flight under the current
+// its own 32-k chunks in LDS (k-major), the next chunk's global loads in flight under the current
 // chunk's FMAs; the groups' partials meet in LDS and group 0 adds them in quarter order.
 // (Round 4's one-chain kernel ran 16 x 64 tiles over all of k per thread: 110-190 us per R50 slice
 // of 128 images, a fifth of the chip busy; this one splits the chain four ways over 4x the blocks.)
-constexpr int kFcI = 8, kFcO = 64, kFcK = 64, kFcG = 4;
+constexpr int kFcI = 8, kFcO = 64, kFcK = 32, kFcG = 4;
+constexpr int kFcKQ = kFcK / 4;  // float4 per staged row
 __global__ __launch_bounds__(512) void fc_kernel(const float* __restrict__ pooled, int n, int c,
                                                  const float* __restrict__ w, const float* __restrict__ b, int nout,
                                                  float* __restrict__ logits) {
@@ -156,37 +157,38 @@ __global__ __launch_bounds__(512) void fc_kernel(const float* __restrict__ poole
   const int grp = threadIdx.x >> 7, tid = threadIdx.x & 127;
   const int i0 = blockIdx.y * kFcI, o0 = blockIdx.x * kFcO;
   const int ti = tid / 16, to = tid % 16;
-  // quarter ranges: whole 64-k chunks, fixed by c
+  // quarter ranges: whole kFcK chunks, fixed by c
   const int cq = ((c + kFcG - 1) / kFcG + kFcK - 1) / kFcK * kFcK;
   const int kb = min(c, grp * cq), ke = min(c, kb + cq);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  // staging: pooled 8 images x 64 k (one float4 per thread of the group); weights 64 x 64 k
-  // (eight float4 per thread)
-  float4 vp, vw[8];
+  // staging: pooled kFcI images x kFcK k (one float4 per thread of the group's first kFcI * kFcKQ);
+  // weights kFcO x kFcK k (kFcO * kFcKQ / 128 float4 per thread)
+  constexpr int kWR = kFcO * kFcKQ / 128;
+  float4 vp, vw[kWR];
   auto load = [&](int k0) {
     {
-      const int ii = tid / 16, kq = tid % 16, img = i0 + ii, k = k0 + 4 * kq;
-      vp = (tid < 128 && img < n && k < ke) ? *reinterpret_cast<const float4*>(pooled + (long long)img * c + k)
+      const int ii = tid / kFcKQ, kq = tid % kFcKQ, img = i0 + ii, k = k0 + 4 * kq;
+      vp = (tid < kFcI * kFcKQ && img < n && k < ke) ? *reinterpret_cast<const float4*>(pooled + (long long)img * c + k)
                                            : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int e = tid + 128 * r, oo = e / 16, kq = e % 16, o = o0 + oo, k = k0 + 4 * kq;
+    for (int r = 0; r < kWR; ++r) {
+      const int e = tid + 128 * r, oo = e / kFcKQ, kq = e % kFcKQ, o = o0 + oo, k = k0 + 4 * kq;
       vw[r] = (o < nout && k < ke) ? *reinterpret_cast<const float4*>(w + (long long)o * c + k)
                                    : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
   auto store = [&]() {
-    {
-      const int ii = tid / 16, kq = tid % 16;
+    if (tid < kFcI * kFcKQ) {
+      const int ii = tid / kFcKQ, kq = tid % kFcKQ;
       sp[grp][4 * kq][ii] = vp.x;
       sp[grp][4 * kq + 1][ii] = vp.y;
       sp[grp][4 * kq + 2][ii] = vp.z;
       sp[grp][4 * kq + 3][ii] = vp.w;
     }
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int e = tid + 128 * r, oo = e / 16, kq = e % 16;
+    for (int r = 0; r < kWR; ++r) {
+      const int e = tid + 128 * r, oo = e / kFcKQ, kq = e % kFcKQ;
       sw[grp][4 * kq][oo] = vw[r].x;
       sw[grp][4 * kq + 1][oo] = vw[r].y;
       sw[grp][4 * kq + 2][oo] = vw[r].z;

@@ -40,8 +40,8 @@ for step in "$@"; do
     trace)
       run 300 $o.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof -o run -- \
         python3 bench.py --no-cpu-baseline
-      f=$(ls gpurun_out/${tag}_prof/*/run_kernel_stats.csv 2>/dev/null | head -n 1)
-      t=$(ls gpurun_out/${tag}_prof/*/run_kernel_trace.csv 2>/dev/null | head -n 1)
+      f=$(find gpurun_out/${tag}_prof -name run_kernel_stats.csv | head -n 1)
+      t=$(find gpurun_out/${tag}_prof -name run_kernel_trace.csv | head -n 1)
       python tools/rocprof_summary.py "$f" "$t" > $o.summary.txt 2>&1
       python tools/graph_region.py "$t" > $o.graph.txt 2>&1
       ;;
