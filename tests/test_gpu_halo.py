@@ -108,7 +108,7 @@ def test_model_forward_halo_tiles_bitwise(gpu, arch, assign):
     picked = []
 
     def choose(kind):
-        def pick(key, run, cands):
+        def pick(key, run, cands, variant=None):
             halo = [c for c in cands if ops.tile_kind(c) == ops.TILE_HALO3X3]
             gemm = [c for c in cands if ops.tile_kind(c) != ops.TILE_HALO3X3]
             # a halo tile only where the call is one it runs (lean, ReLU): key = n|h|w|cin|cout|kh|kw|
