@@ -134,16 +134,29 @@ class ConvTimer:
         }
 
 
-def attach_traffic(roof, config, limbs, batch):
+def attach_traffic(roof, config, limbs, batch, streams):
     """roofline.traffic: HBM bytes per quantized-conv launch from the committed PMC measurement of
     this workload (tools/pmc_traffic.sh: FETCH_SIZE and WRITE_SIZE passes of rocprofv3 over this
     bench's eager roofline region, gfx950-corrected by tools/pmc_traffic.py). PMC counters cannot
-    be read from inside a normal run, so the number comes from that profile; null if absent."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic_%s_L%d_B%d.json" % (config, limbs, batch))
+    be read from inside a normal run, so the number comes from that profile. It is attached only
+    when the profile was taken on this very library (build stamp), tile table (content hash) and
+    launch layout; otherwise traffic is null and roofline.traffic_note says why."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic_%s_L%d_B%d_S%d.json" % (config, limbs, batch, streams))
     if not os.path.exists(path):
+        roof["traffic_note"] = "no PMC profile " + os.path.relpath(path, REPO)
         return
     m = json.load(open(path))
+    from smpq import _lib, ops
+    stamp = _lib.load().smpq_build_stamp().decode()
+    why = []
+    if m.get("lib_stamp") != stamp:
+        why.append("library build stamp %s != %s" % (str(m.get("lib_stamp"))[:16], stamp[:16]))
+    if m.get("tile_table_sha16") != ops.tile_table_info()["sha16"]:
+        why.append("tile table %s != %s" % (m.get("tile_table_sha16"), ops.tile_table_info()["sha16"]))
     if m.get("launches") != roof["launches_per_step"] * m.get("rsteps", 3):
+        why.append("launches %s != %d" % (m.get("launches"), roof["launches_per_step"] * m.get("rsteps", 3)))
+    if why:
+        roof["traffic_note"] = "stale PMC profile (%s): %s" % (os.path.basename(path), "; ".join(why))
         return
     roof["traffic"] = m["traffic_bytes_per_launch"]
     roof["traffic_over_alg_bytes"] = round(m["traffic_bytes_per_launch"] / roof["alg_bytes_per_launch"], 4)
@@ -291,30 +304,51 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    # per-launch kernel times for the roofline: the same forward, launched eagerly
-    timer = ConvTimer()
+    # per-launch kernel durations for the roofline: the same forward, launched eagerly, one launch
+    # at a time (events time each kernel alone). Region 1: the whole batch per launch (for
+    # reference); region 2 (last, so that tools/pmc_traffic.sh's PMC passes see it as the last
+    # dispatches): the timed path's own batch slices and tile choices, the slices run one after
+    # the other on one stream. The roofline line reports region 2.
     use_graph, conc, nst = engine.USE_GRAPH[0], engine.CONCURRENT_DS[0], engine.STREAMS[0]
-    engine.USE_GRAPH[0] = False
-    engine.CONCURRENT_DS[0] = False  # one launch at a time: events time each kernel alone
-    engine.STREAMS[0] = 1
-    ops.set_conv_hook(timer)
-    step()  # untimed: the eager path's first pass
-    timer.active = True
-    for _ in range(args.roofline_steps):
-        step()
-    timer.active = False
-    ops.set_conv_hook(None)
-    engine.USE_GRAPH[0], engine.CONCURRENT_DS[0], engine.STREAMS[0] = use_graph, conc, nst
+
+    def eager_region(streams):
+        timer = ConvTimer()
+        engine.USE_GRAPH[0] = False
+        engine.CONCURRENT_DS[0] = False
+        engine.STREAMS[0] = streams
+        engine.SERIAL_SLICES[0] = True
+        ops.set_conv_hook(timer)
+        step()  # untimed: the eager path's first pass
+        timer.active = True
+        for _ in range(args.roofline_steps):
+            step()
+        timer.active = False
+        ops.set_conv_hook(None)
+        engine.USE_GRAPH[0], engine.CONCURRENT_DS[0], engine.STREAMS[0] = use_graph, conc, nst
+        engine.SERIAL_SLICES[0] = False
+        return timer
+
+    sliced = nst > 1 and args.batch >= 2 * nst
+    whole = eager_region(1) if sliced else None
+    timer = eager_region(nst)
     lockstep.close()
     roof = timer.roofline(args.roofline_steps)
+    roof["region"] = ("the timed path's %d batch slices of %d images per launch and its tile choices, one launch at "
+                      "a time" % (nst, -(-args.batch // nst))) if sliced else \
+        "the whole batch of %d images per launch, one launch at a time" % args.batch
+    if whole is not None:
+        rw = whole.roofline(args.roofline_steps)
+        roof["whole_batch"] = {k: rw[k] for k in ("frac", "achieved", "avg_launch_ms", "launches_per_step",
+                                                   "conv_ms_per_step", "mfma_frac_incl_limb_passes")}
+        roof["whole_batch"]["region"] = "the whole batch of %d images per launch, one launch at a time" % args.batch
     if args.layers and rank == 0:
-        timer.print_layers(args.roofline_steps)
+        (whole or timer).print_layers(args.roofline_steps)
 
     images = args.batch * world * args.steps
     value = images / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     roof["kernel_share_of_step"] = round(roof["conv_ms_per_step"] / ms_per_step, 4)
-    attach_traffic(roof, args.config, args.limbs, args.batch)
+    attach_traffic(roof, args.config, args.limbs, args.batch, nst if sliced else 1)
     if rank == 0:
         res = {
             "metric": METRIC,

@@ -230,6 +230,8 @@ def run_conv(conv, bn, act, relu, residual=None, want_amax=True, ctx=None, want_
 _STREAMS = {}
 
 
+# measurement (bench.py): run the batch slices one after another on the current stream
+SERIAL_SLICES = [False]
 # diagnostics: the first batch slice's stream at high priority (the others at normal priority)
 SLICE_PRIORITY = [_os.environ.get("SMPQ_SLICE_PRIORITY", "0") != "0"]
 
@@ -419,7 +421,9 @@ def _forward(model, x, ctx):
         for i in range(lanes):
             _stream((x.device, "slice", i)).wait_stream(main)
         for i, (s0, s1) in enumerate(parts):
-            with torch.cuda.stream(_stream((x.device, "slice", i % lanes))):
+            # SERIAL_SLICES (bench.py's roofline region): the same slices and launches, one after
+            # another on the current stream, so that per-launch events time each kernel alone
+            with torch.cuda.stream(main if SERIAL_SLICES[0] else _stream((x.device, "slice", i % lanes))):
                 ctx.n, ctx.lane = s1 - s0, i % lanes
                 logits.append(_head(model, _features(model, x[s0:s1], ctx)))
         for i in range(lanes):

@@ -11,7 +11,11 @@ The launches compared are the last `rsteps x launches` quantized-conv dispatches
 event-timed eager roofline region — so the traffic and `roofline.achieved` cover the same
 kernels. Writes profiles/<out>.json, which bench.py copies into roofline.traffic.
 
-usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [launches_per_step] [rsteps]
+The profile is bound to what it measured: the library's build stamp, the tile table's content
+hash and the launch layout (launches per step) are stored with it, and bench.py attaches it only
+when all three match the running bench (otherwise roofline.traffic is null).
+
+usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> <bench_log> [rsteps]
 """
 import csv
 import glob
@@ -30,10 +34,21 @@ def per_dispatch(d, counter):
     return [rows[k] for k in sorted(rows)]
 
 
+def bench_line(log):
+    """The bench's JSON result line in its log (the PMC pass's own run)."""
+    for line in reversed(open(log).read().splitlines()):
+        if line.startswith("{") and '"roofline"' in line:
+            return json.loads(line)
+    raise SystemExit("no bench result line in " + log)
+
+
 def main():
-    fetch_dir, write_dir, out = sys.argv[1:4]
-    per_step = int(sys.argv[4]) if len(sys.argv) > 4 else 53
+    fetch_dir, write_dir, out, log = sys.argv[1:5]
     rsteps = int(sys.argv[5]) if len(sys.argv) > 5 else 3
+    b = bench_line(log)
+    per_step = b["roofline"]["launches_per_step"]
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import __graft_entry__
     n = per_step * rsteps
     fe = per_dispatch(fetch_dir, "FETCH_SIZE")[-n:]
     wr = per_dispatch(write_dir, "WRITE_SIZE")[-n:]
@@ -43,6 +58,9 @@ def main():
     res = {
         "launches": n,
         "rsteps": rsteps,
+        "lib_stamp": __graft_entry__.library_stamp(),
+        "tile_table_sha16": b["config"]["tile_table"]["sha16"],
+        "region": b["roofline"].get("region"),
         "fetch_bytes_per_launch": round(sum(fetch) / n),
         "write_bytes_per_launch": round(sum(write) / n),
         "traffic_bytes_per_launch": round((sum(fetch) + sum(write)) / n),
