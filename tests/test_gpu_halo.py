@@ -18,7 +18,11 @@ def _halo_cfgs(ops, limbs, cin, cout):
 @pytest.mark.parametrize("relu", [True, False])
 @pytest.mark.parametrize("limbs", [2, 3])
 @pytest.mark.parametrize("shape", [(64, 64, 56, 56, 2), (128, 128, 28, 28, 3), (256, 256, 14, 14, 2),
-                                   (64, 128, 13, 17, 2), (192, 64, 9, 30, 1)],
+                                   (64, 128, 13, 17, 2), (192, 64, 9, 30, 1),
+                                   # the virtual-row tiles' geometries: two 7 x 7 images per tile
+                                   # (an odd image count leaves half a tile empty), one image of
+                                   # width 16 / narrower than 7 / a partial row tile
+                                   (512, 512, 7, 7, 3), (64, 128, 9, 16, 2), (128, 64, 5, 6, 3)],
                          ids=lambda s: "c%d_o%d_%dx%d_n%d" % s)
 def test_halo_equals_implicit_gemm(gpu, shape, limbs, relu):
     from smpq import _lib, ops
@@ -46,9 +50,12 @@ def test_halo_equals_implicit_gemm(gpu, shape, limbs, relu):
                         ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=relu, tile_cfg=c,
                                      emit_range=rng, overflow=ovf, want_f32=False, weight_layout=layout)
                     continue
-                yq = torch.full_like(yq0, 0x5a)  # every element must be written
-                _, yq = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=relu, tile_cfg=c,
-                                     emit_range=rng, overflow=ovf, want_f32=False, weight_layout=layout)
+                try:
+                    _, yq = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=relu, tile_cfg=c,
+                                         emit_range=rng, overflow=ovf, want_f32=False, weight_layout=layout)
+                except _lib.SmpqError as e:  # a virtual-row tile refuses images wider than its slots
+                    assert "too wide" in str(e) and ops.tile_configs()[c][0] % 16 == 0 and w > 7, (c, e)
+                    continue
                 assert torch.equal(yq, yq0), (c, frac, layout)
                 assert torch.equal(ovf, ovf0), (c, frac, layout)
 
@@ -103,7 +110,8 @@ def test_model_forward_halo_tiles_bitwise(gpu, arch, assign):
     from smpq import engine, ops
     from test_gpu import build_model
     net = build_model(gpu, arch, assign, None)
-    x = torch.randn(4, 3, 224, 224, generator=torch.Generator().manual_seed(7)).to(gpu)
+    x = torch.randn(5, 3, 224, 224, generator=torch.Generator().manual_seed(7)).to(gpu)
+    vrow = [c for c, v in ops.tile_configs().items() if ops.tile_kind(c) == ops.TILE_HALO3X3 and v[0] == 112]
     orig = ops._choose_tile
     picked = []
 
@@ -115,8 +123,11 @@ def test_model_forward_halo_tiles_bitwise(gpu, arch, assign):
             # stride|pad|limbs|wlimbs|res_f32|emit_q|want_f32|res_q
             lean = key[5] == 3 and key[7] == 1 and key[12] and not key[13] and not key[14] and not key[11]
             if kind == "halo" and halo and lean:
-                picked.append(halo[0])
-                return halo[0]
+                # the virtual-row tiles where the images fit them (conv_halo.hip kHaloV order: one
+                # image up to 16 wide, then two images up to 7 wide)
+                c = vrow[1] if key[2] <= 7 else vrow[0] if key[2] <= 16 else halo[0]
+                picked.append(c)
+                return c
             return gemm[0] if gemm else None
         return pick
 
@@ -135,4 +146,5 @@ def test_model_forward_halo_tiles_bitwise(gpu, arch, assign):
         ops._TUNED.clear()
         engine.USE_GRAPH[0] = True
     assert picked, "no conv ran on a halo tile"
+    assert any(c in vrow for c in picked), "no conv ran on a virtual-row halo tile"
     assert torch.equal(outs["halo"], outs["gemm"])
