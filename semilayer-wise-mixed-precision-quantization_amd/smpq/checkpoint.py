@@ -67,6 +67,8 @@ def save_checkpoint(net, path, plain=True):
     """``torch.save(net.state_dict(), path)`` + ``<path>.bits.json`` (bits + exact steps). With
     ``plain`` the .pth carries the reference's keys only (loadable with strict=True by the
     reference's / torchvision's ResNet); otherwise it also keeps the qbits/qstep buffers."""
+    from .quant import check_pending
+    check_pending()
     torch.save(plain_state_dict(net) if plain else net.state_dict(), path)
     side = {"format": "smpq-bits/2", "convs": {str(k): v for k, v in bit_assignment(net).items()},
             "steps": {str(k): v for k, v in step_assignment(net).items()}}

@@ -49,6 +49,7 @@ import torch.nn.functional as F
 from . import ops
 from .fingerprint import Fingerprinter
 from .qconv import QConv2d, stats
+from .quant import check_pending
 
 import os as _os
 # "dynamic" is the deterministic mode for search runs (each image's logits depend on nothing but
@@ -723,6 +724,7 @@ def _dynamic_forward(model, x):
 
 def forward_fused(model, x):
     """Eval-mode forward of an smpq ResNet on the GPU; returns logits [n, num_classes]."""
+    check_pending()  # a deferred per-channel quantization that met a constant channel raises here
     if _MODE[0] == "dynamic":
         return _dynamic_forward(model, x)
     if torch.cuda.is_current_stream_capturing():

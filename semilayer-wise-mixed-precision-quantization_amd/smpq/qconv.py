@@ -37,12 +37,20 @@ def _storage_key(t):
     return (t.device.type, t.device.index, t.untyped_storage().data_ptr())
 
 
+_OWNERS = {}  # storage key -> weakref of the QConv2d found last for it (verified on every hit)
+
+
 def find_owner(tensor):
     """The QConv2d whose weight shares storage with ``tensor`` (None if not a QConv2d weight)."""
     key = _storage_key(tensor)
+    ref = _OWNERS.get(key)
+    m = ref() if ref is not None else None
+    if m is not None and m.weight.device == tensor.device and _storage_key(m.weight.data) == key:
+        return m
     for m in list(_REGISTRY):
         w = m.weight
         if w.device == tensor.device and _storage_key(w.data) == key:
+            _OWNERS[key] = weakref.ref(m)
             return m
     return None
 
@@ -70,6 +78,13 @@ class QConv2d(nn.Conv2d):
         self.qbits[idx.to(self.qbits.device)] = int(bit)
         self.qstep[idx.to(self.qstep.device)] = step.reshape(-1).to(self.qstep.device)
         self._bits_host[idx.numpy()] = int(bit)
+        self._meta_gen += 1
+
+    def record_quant_inplace(self, channel, bit):
+        """record_quant for one channel whose step the quantizer kernel already wrote into
+        ``qstep[channel]`` (smpq.quant's deferred path): the bit-width as a device fill, no upload."""
+        self.qbits[channel] = bit
+        self._bits_host[channel] = bit
         self._meta_gen += 1
 
     def record_quant_all(self, bits_host, step):

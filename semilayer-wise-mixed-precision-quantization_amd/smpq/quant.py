@@ -6,10 +6,67 @@ libsmpq.so), and additionally record the (bit, step) metadata on the owning QCon
 of functions.py:41 follows where the tensor lives, as the reference's own result does (torch
 divides on the CPU and multiplies by a reciprocal on the GPU; ops.set_quant_semantics).
 """
+import os
+
 import torch
 
-from . import ops
+from . import _lib, ops
 from .qconv import find_owner
+
+# The unmodified search drivers call channel_wise_quantizationperchan once per CHANNEL
+# (resnet50_main.py:189-197): a host sync per call for the constant-channel check, a bits upload
+# and the metadata index writes cost ~140 us per call, 5.5 % of a driver step
+# (profiles/r05_driver_quant_cost.json). With DEFER (default) a device weight's channel is
+# quantized by one launch with no host sync: the bit-width comes from a device-resident table,
+# the step is written straight into the owning conv's qstep, and a constant channel (the
+# reference raises ZeroDivisionError at functions.py:40, leaving it untouched — so does the
+# kernel) is recorded in a per-device flag that check_pending() reads: at the start of the next
+# forward (smpq.engine.forward_fused), evaluation or checkpoint save, which raise the
+# ZeroDivisionError there. SMPQ_QUANT_DEFER=0 restores the synchronous check per call.
+DEFER = [os.environ.get("SMPQ_QUANT_DEFER", "1") != "0"]
+_DEV = {}  # device -> {"bits": int8 [17] = 0..16, "status": int32 [1], "scratch": fp32 [1], "pending": n}
+
+
+def _dev_state(device):
+    st = _DEV.get(device)
+    if st is None:
+        st = _DEV[device] = {"bits": torch.arange(17, dtype=torch.int8, device=device),
+                             "status": torch.zeros(1, dtype=torch.int32, device=device),
+                             "scratch": torch.zeros(1, dtype=torch.float32, device=device), "pending": 0}
+    return st
+
+
+def check_pending(device=None):
+    """Raise ZeroDivisionError if a deferred channel_wise_quantizationperchan call (on ``device``,
+    or any) met a constant channel (functions.py:40). One host sync, and only while calls are
+    pending; the flag is cleared either way."""
+    for dev, st in list(_DEV.items()):
+        if (device is not None and dev != device) or not st["pending"]:
+            continue
+        n, st["pending"] = st["pending"], 0
+        if int(st["status"].item()):
+            st["status"].zero_()
+            raise ZeroDivisionError("float division by zero (a constant channel in one of the last %d "
+                                    "channel_wise_quantizationperchan calls, functions.py:40)" % n)
+
+
+def _quantize_row_deferred(tensor, bit, i):
+    """One channel of a contiguous fp32 device weight, no host sync (see DEFER)."""
+    row = tensor[i]
+    st = _dev_state(tensor.device)
+    owner = find_owner(tensor)
+    if owner is not None and owner.qstep.device != tensor.device:
+        owner = None
+    step = owner.qstep[i:i + 1] if owner is not None else st["scratch"]
+    lib = _lib.load()
+    with torch.cuda.device(tensor.device):
+        _lib.check(lib.smpq_quantize_channels_ex(_lib.ptr(row), 1, row.numel(), st["bits"].data_ptr() + int(bit),
+                                                 _lib.ptr(step), _lib.ptr(st["status"]), ops._qsem(None, True),
+                                                 _lib.stream_ptr()), "smpq_quantize_channels_ex")
+    st["pending"] += 1
+    if owner is not None:
+        owner.record_quant_inplace(int(i), int(bit))  # qstep[i] was written by the kernel
+    return tensor
 
 
 def quantize_wgt(tensor, bit):
@@ -22,6 +79,9 @@ def quantize_wgt(tensor, bit):
 
 def channel_wise_quantizationperchan(tensor, bit, i):
     """functions.py:9-23: quantize channel ``i`` of ``tensor`` IN PLACE; returns ``tensor``."""
+    if DEFER[0] and tensor.is_cuda and tensor.dtype == torch.float32 and 1 <= int(bit) <= 16 \
+            and tensor[i].is_contiguous():
+        return _quantize_row_deferred(tensor, bit, i)
     row = tensor[i]
     if tensor.dtype == torch.float32 and row.is_contiguous():
         step = ops.quantize_channels_(row.reshape(1, -1), [int(bit)])

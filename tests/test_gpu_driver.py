@@ -116,3 +116,48 @@ def test_evaluation_history_independent(gpu):
         assert r[0] == r1[0] and r[1] == r1[1]
         for a, b in zip(r[2], r1[2]):
             assert torch.equal(a, b)
+
+
+def test_deferred_channel_quantizer(gpu):
+    """The drop-in per-channel quantizer on device weights runs without a host sync per call
+    (smpq.quant.DEFER): each call gives the same weight bits, recorded step and bit-width as the
+    synchronous quantizer, and a constant channel leaves its weights untouched and raises the
+    reference's ZeroDivisionError (functions.py:40) at the next forward instead of in the call."""
+    import functions
+    from smpq import ops, quant
+    net = build_model(gpu, "resnet18", None)
+    conv = net.layer3[1].conv1
+    w0 = conv.weight.detach().clone()
+    chans = list(range(0, conv.out_channels, 3))
+    for c in chans:
+        conv.weight.data = functions.channel_wise_quantizationperchan(conv.weight.data, 6 if c % 2 else 4, c)
+    ref = w0.reshape(conv.out_channels, -1).clone()
+    bits = [0] * conv.out_channels
+    for c in chans:
+        bits[c] = 6 if c % 2 else 4
+    step = ops.quantize_channels_(ref, bits, semantics="device")
+    assert torch.equal(conv.weight.detach().reshape(conv.out_channels, -1), ref)
+    assert torch.equal(conv.qstep, step) and conv.qbits.tolist() == bits
+    assert int(conv._bits_host.sum()) == sum(bits)
+    quant.check_pending()  # nothing to report
+    x = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(4)).to(gpu)
+    with torch.no_grad():
+        net(x)
+    # a constant channel: no error in the call, the channel untouched, the error at the next forward
+    conv2 = net.layer4[0].conv2
+    with torch.no_grad():
+        conv2.weight.data[7] = 0.25
+    before = conv2.weight.detach().clone()
+    functions.channel_wise_quantizationperchan(conv2.weight.data, 8, 7)
+    with pytest.raises(ZeroDivisionError):
+        with torch.no_grad():
+            net(x)
+    assert torch.equal(conv2.weight.detach()[7], before[7])
+    quant.check_pending()  # cleared by the raise
+    # the synchronous path (DEFER off) raises in the call, as the reference does
+    quant.DEFER[0] = False
+    try:
+        with pytest.raises(ZeroDivisionError):
+            functions.channel_wise_quantizationperchan(conv2.weight.data, 8, 7)
+    finally:
+        quant.DEFER[0] = True
