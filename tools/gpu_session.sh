@@ -42,7 +42,7 @@ for step in "$@"; do
         python3 bench.py --no-cpu-baseline
       f=$(find gpurun_out/${tag}_prof -name run_kernel_stats.csv | head -n 1)
       t=$(find gpurun_out/${tag}_prof -name run_kernel_trace.csv | head -n 1)
-      python tools/rocprof_summary.py "$f" "$t" > $o.summary.txt 2>&1
+      python tools/rocprof_summary.py "$f" "$t" 106 > $o.summary.txt 2>&1
       python tools/graph_region.py "$t" > $o.graph.txt 2>&1
       ;;
     traffic) run 600 $o.log bash tools/pmc_traffic.sh r50_mixed 3 256 ;;

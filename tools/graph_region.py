@@ -3,12 +3,15 @@
 
 usage: python tools/graph_region.py <run_kernel_trace.csv> [launches_per_slice steps rsteps slices]
 
-bench.py's tail in the trace: [timed: steps graph replays, each `slices` batch slices of
-`launches_per_slice` quantized convs on their own queues] [1 untimed eager step] [rsteps eager
-roofline steps]. A slice is a dependency chain (its kernels never overlap each other); the
-chains run concurrently, one per hardware queue (Queue_Id). For each layer: the mean duration
-in the graph region (concurrent with the other slice), the duration of the same layer in the
-eager roofline region, and the step's wall time vs the summed kernel time per chain.
+bench.py's tail in the trace (round 5): [timed: steps graph replays, each `slices` batch slices
+of `launches_per_slice` quantized convs on their own queues] [whole-batch eager region: 1 + rsteps
+steps] [roofline region: 1 + rsteps steps of the same slices, one launch at a time]. A slice is a
+dependency chain (its kernels never overlap each other); the chains run concurrently, one per
+hardware queue (Queue_Id). For each layer: the mean duration in the graph region (concurrent with
+the other slice), the duration of the same layer launched alone in the roofline region, and the
+step's wall time vs the summed kernel time per chain. NB: rocprofv3's per-dispatch overhead
+delays the second slice's start in a traced replay (~2 ms); tools/timeline_probe.py measures the
+timeline without a profiler.
 """
 import collections
 import csv
@@ -32,8 +35,8 @@ def main():
     slices = int(sys.argv[5]) if len(sys.argv) > 5 else 2
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     q = [r for r in rows if "qconv" in r["Kernel_Name"]]
-    eager_n = (rsteps + 1) * per
-    roof = q[-rsteps * per:]
+    eager_n = (rsteps + 1) * per + (rsteps + 1) * per * slices
+    roof = q[-rsteps * per * slices:]
     timed = q[-eager_n - steps * per * slices:-eager_n]
     if len(timed) != steps * per * slices:
         raise SystemExit("trace too short for %d steps" % steps)
@@ -54,7 +57,7 @@ def main():
             for i, r in enumerate(c):
                 lay[i].append((dur(r), short(r["Kernel_Name"]), r["Grid_Size_X"], r["Workgroup_Size_X"]))
     rl = collections.defaultdict(list)
-    for k in range(rsteps):
+    for k in range(rsteps * slices):
         for i, r in enumerate(roof[k * per:(k + 1) * per]):
             rl[i].append(dur(r))
     print("%3s %9s %9s %6s  %-60s %9s %5s" % ("#", "graph_us", "eager_us", "ratio", "kernel (graph slice)", "grid", "wg"))
@@ -71,7 +74,7 @@ def main():
     b = sorted(busy)[len(busy) // 2]
     print("graph region: median step wall %.1f us (qconv span), qconv time per slice chain %.1f us "
           "(sum over the %d chains %.1f us, concurrency %.2f)" % (w, b, slices, b * slices, b * slices / w))
-    print("per slice: sum of graph-region layer means %.1f us; eager roofline region (whole batch, serial) %.1f us"
+    print("per slice: sum of graph-region layer means %.1f us; roofline region (the same slice launched alone) %.1f us"
           % (tg, te))
 
 

@@ -26,6 +26,20 @@ import __graft_entry__  # noqa: E402
 ARCH = {"r50_mixed": "resnet50", "r18_u8": "resnet18", "r34_4bit": "resnet34"}
 
 
+def table_entries(ops):
+    """The table's entries from the tuner's cache. A cache key is the call key, or (call key,
+    "nohalo") for calls the halo tiles cannot run (ops.tuned_conv2d_q); the table stores call keys,
+    so where both forms were tuned the halo-eligible call's winner is kept (the other call then
+    finds it outside its candidates and is tuned at run time)."""
+    tiles = {}
+    for k, v in ops._TUNED.items():
+        base, variant = (k[0], k[1]) if (isinstance(k, tuple) and len(k) == 2 and isinstance(k[0], tuple)) else (k, None)
+        ks = ops.key_str(base)
+        if variant is None or ks not in tiles:
+            tiles[ks] = int(v)
+    return dict(sorted(tiles.items()))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=25)
@@ -62,7 +76,7 @@ def main():
                      "workloads %s" % (args.reps, args.configs),
            "key": "tuned_conv2d_q: n|h|w|cin|cout|kh|kw|stride|pad|limbs|wlimbs|res_f32|emit_q|want_f32|res_q; "
                   "tuned_stem_conv_s2d: stem_s2d|planes|codes|h|w|y_absmax|emit_q|want_f32",
-           "tiles": {ops.key_str(k): int(v) for k, v in sorted(ops._TUNED.items(), key=lambda kv: ops.key_str(kv[0]))}}
+           "tiles": table_entries(ops)}
     with open(out, "w") as f:
         json.dump(doc, f, indent=1, sort_keys=False)
         f.write("\n")
