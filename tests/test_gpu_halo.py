@@ -63,7 +63,7 @@ def test_halo_equals_implicit_gemm(gpu, shape, limbs, relu):
 def test_halo_without_offsets_and_repeatable(gpu):
     """No weight offsets (the plain-code path) and 20 back-to-back launches of every halo config
     give the same bits (no race between the DMA of one chunk and the reads of the last)."""
-    from smpq import ops
+    from smpq import _lib, ops
     cin, cout, h = 128, 64, 28
     wd, step, codes, offset = make_layer(gpu, cin, cout, 3, seed=11, bits_choice=(6, 4))
     x = torch.relu(torch.randn(4, h, h, cin, generator=torch.Generator().manual_seed(3))).to(gpu)
@@ -76,9 +76,41 @@ def test_halo_without_offsets_and_repeatable(gpu):
     _, yq0 = ops.conv2d_q(xq, am, codes, None, 3, 3, 1, 1, step, shift, relu=True, emit_range=rng, overflow=ovf,
                           want_f32=False)
     for c in _halo_cfgs(ops, 3, cin, cout):
+        try:
+            ops.conv2d_q(xq, am, codes, None, 3, 3, 1, 1, step, shift, relu=True, tile_cfg=c, emit_range=rng,
+                         overflow=ovf, want_f32=False)
+        except _lib.SmpqError as e:  # virtual-row tiles take images up to 16 (7) wide only
+            assert "too wide" in str(e), (c, e)
+            continue
         outs = [ops.conv2d_q(xq, am, codes, None, 3, 3, 1, 1, step, shift, relu=True, tile_cfg=c, emit_range=rng,
                              overflow=ovf, want_f32=False)[1] for _ in range(20)]
         for yq in outs:
+            assert torch.equal(yq, yq0), c
+    assert int(ovf.item()) == 0
+
+
+@pytest.mark.parametrize("h", [14, 7])
+def test_vrow_halo_repeatable(gpu, h):
+    """The virtual-row tiles at 14^2 (one image per tile) and 7^2 (two images per tile, an odd
+    image count): 20 back-to-back launches give the implicit-GEMM kernel's bits every time."""
+    from smpq import ops
+    cin, cout, n = 256, 128, 5
+    wd, step, codes, offset = make_layer(gpu, cin, cout, 3, seed=h)
+    x = torch.relu(torch.randn(n, h, h, cin, generator=torch.Generator().manual_seed(h))).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, 3)
+    shift = torch.linspace(-0.5, 0.5, cout, device=gpu)
+    ref = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=True)
+    rng = float(ref.abs().max()) * 2
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+    _, yq0 = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=True, emit_range=rng, overflow=ovf,
+                          want_f32=False)
+    vrow = [c for c, v in ops.tile_configs().items() if ops.tile_kind(c) == ops.TILE_HALO3X3 and v[0] == 112]
+    assert len(vrow) == 4
+    for c in vrow:
+        for _ in range(20):
+            _, yq = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=True, tile_cfg=c,
+                                 emit_range=rng, overflow=ovf, want_f32=False)
             assert torch.equal(yq, yq0), c
     assert int(ovf.item()) == 0
 
