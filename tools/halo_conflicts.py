@@ -6,7 +6,12 @@ row-major order), every tap (kr, kc) and every ds_read_b128 lane group of gfx950
 LDS cycles of the patch image pixel (pr, pc) at (pr * PW + pc) * 64 with 16-B chunk c stored at
 c ^ 2 * (pr & 1). Pure host arithmetic, no GPU.
 
-    python tools/halo_conflicts.py"""
+--vrow: the virtual-row tiles (conv_halo.hip qconv_halo_vrow_kernel): fragment f = one 16-lane row,
+lane v reads patch pixel (f + kr, v + kc) of an 18-column patch, chunk c stored at
+c ^ 2 * ((col >> 2) & 1).
+
+    python tools/halo_conflicts.py [--vrow]"""
+import sys
 
 GROUPS = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
           list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
@@ -41,7 +46,22 @@ def tile_conflicts(th, tw, swizzle=True):
     return worst
 
 
+def vrow_conflicts():
+    worst = 0
+    for row in range(9):
+        for kc in range(3):
+            def addr(lane):
+                v, g = lane & 15, lane >> 4
+                j = v + kc
+                return (row * 18 + j) * 64 + 16 * (g ^ (2 * ((j >> 2) & 1)))
+            worst = max(worst, extra_cycles(addr))
+    return worst
+
+
 if __name__ == "__main__":
+    if "--vrow" in sys.argv:
+        print("virtual-row tiles: extra cycles per read, worst case over rows and taps: %d" % vrow_conflicts())
+        sys.exit(0)
     # the kernel's tile shapes (conv_halo.hip kHalo)
     for th, tw in ((8, 8), (16, 8), (28, 4), (14, 4), (7, 14)):
         print("tile %2d x %2d: extra cycles per read, worst case: %d (unswizzled: %d)"
