@@ -10,6 +10,12 @@ from test_gpu import make_layer
 pytestmark = pytest.mark.gpu
 
 
+def _vrow_cfgs(ops):
+    """The virtual-row halo configs: the last four halo tile configs (conv_halo.hip kHaloV follows
+    kHalo): one image up to 16 wide, two images up to 7 wide, and both with a prefetched chunk."""
+    return sorted(c for c in ops.tile_configs() if ops.tile_kind(c) == ops.TILE_HALO3X3)[-4:]
+
+
 def _halo_cfgs(ops, limbs, cin, cout):
     return [c for c in ops.tile_configs()
             if ops.tile_kind(c) == ops.TILE_HALO3X3 and ops._tile_fits(c, limbs, 1, cout, cin, 3)]
@@ -54,7 +60,7 @@ def test_halo_equals_implicit_gemm(gpu, shape, limbs, relu):
                     _, yq = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=relu, tile_cfg=c,
                                          emit_range=rng, overflow=ovf, want_f32=False, weight_layout=layout)
                 except _lib.SmpqError as e:  # a virtual-row tile refuses images wider than its slots
-                    assert "too wide" in str(e) and ops.tile_configs()[c][0] % 16 == 0 and w > 7, (c, e)
+                    assert "too wide" in str(e) and c in _vrow_cfgs(ops) and w > 7, (c, e)
                     continue
                 assert torch.equal(yq, yq0), (c, frac, layout)
                 assert torch.equal(ovf, ovf0), (c, frac, layout)
@@ -105,9 +111,9 @@ def test_vrow_halo_repeatable(gpu, h):
     ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
     _, yq0 = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=True, emit_range=rng, overflow=ovf,
                           want_f32=False)
-    vrow = [c for c, v in ops.tile_configs().items() if ops.tile_kind(c) == ops.TILE_HALO3X3 and v[0] == 112]
+    vrow = _vrow_cfgs(ops)
     assert len(vrow) == 4
-    for c in vrow:
+    for c in (vrow if h <= 7 else vrow[0::2]):  # the two-image tiles take images up to 7 wide
         for _ in range(20):
             _, yq = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=True, tile_cfg=c,
                                  emit_range=rng, overflow=ovf, want_f32=False)
@@ -143,7 +149,7 @@ def test_model_forward_halo_tiles_bitwise(gpu, arch, assign):
     from test_gpu import build_model
     net = build_model(gpu, arch, assign, None)
     x = torch.randn(5, 3, 224, 224, generator=torch.Generator().manual_seed(7)).to(gpu)
-    vrow = [c for c, v in ops.tile_configs().items() if ops.tile_kind(c) == ops.TILE_HALO3X3 and v[0] == 112]
+    vrow = _vrow_cfgs(ops)
     orig = ops._choose_tile
     picked = []
 
