@@ -801,8 +801,8 @@ def test_maxpool_limbs_equals_quantized_maxpool(gpu, limbs):
 def test_fused_stem_pool_bitwise(gpu, limbs, nhw):
     """conv1 + bn1 + relu + maxpool in one launch == stem_conv_s2d (static range) + maxpool_limbs,
     bit for bit: every workgroup band split (2 images -> one pooled row per band at 224; 1 image ->
-    16 bands), partial column fragments (w/2 = 18, 110), and the overflow flag with a range that
-    clamps."""
+    16 bands), partial column fragments (w/2 = 18, 110), negative and zero BN scales, and the
+    overflow flag with a range that clamps."""
     from smpq import ops
     n, h, w = nhw
     g = torch.Generator().manual_seed(31 + limbs + h)
@@ -812,7 +812,10 @@ def test_fused_stem_pool_bitwise(gpu, limbs, nhw):
     am = ops.act_absmax(x)
     lw = max(2, limbs)
     codes, wscale = ops.pack_weights_s2d(wt, lw)
-    cs = (wscale * torch.linspace(0.5, 2, 64, device=gpu)).contiguous()
+    # negative scales (a BN with gamma < 0: the epilogue decreases with the conv value, so the fused
+    # kernel, which pools before its epilogue, pools the minimum there) and a zero scale
+    cs = (wscale * torch.linspace(-1.0, 2, 64, device=gpu)).contiguous()
+    cs[5] = 0.0
     sh = torch.linspace(-1, 1, 64, device=gpu).contiguous()
     xs = ops.image_quantize_s2d(x, am, limbs)
     assert ops.stem_pool_supported(xs, codes, h, w)
