@@ -60,7 +60,7 @@ def main():
         "rsteps": rsteps,
         "lib_stamp": __graft_entry__.library_stamp(),
         "tile_table_sha16": b["config"]["tile_table"]["sha16"],
-        "region": b["roofline"].get("region"),
+        "region": b["roofline"].get("isolated", b["roofline"]).get("region"),
         "fetch_bytes_per_launch": round(sum(fetch) / n),
         "write_bytes_per_launch": round(sum(write) / n),
         "traffic_bytes_per_launch": round((sum(fetch) + sum(write)) / n),
