@@ -511,6 +511,12 @@ AUTOTUNE = [os.environ.get("SMPQ_AUTOTUNE", "1") != "0"]
 TUNE_REPS = [int(os.environ.get("SMPQ_TUNE_REPS", "10"))]
 # diagnostics (A/B of tile families on one box): tile configs the autotuner never tries
 TILES_EXCLUDED = {int(c) for c in os.environ.get("SMPQ_TILES_EXCLUDE", "").split(",") if c.strip()}
+# tools/tune_tiles.py --concurrent: time each candidate as TUNE_CONCURRENT copies launched together on
+# their own streams (the timed forward runs its batch slices concurrently, and a tile's isolated time
+# does not predict how it shares the GPU with the other slice's kernels); TUNE_LOG keeps every
+# candidate's median per key
+TUNE_CONCURRENT = [1]
+TUNE_LOG = {}
 _TUNED = {}
 TILE_TABLE_DEFAULT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "tiles_gfx950.json")
 _TABLE = {"path": None, "sha16": None, "entries": {}, "hits": 0, "tuned": 0}
@@ -565,17 +571,32 @@ def _choose_tile(key, run, cands, variant=None):
     if not AUTOTUNE[0] or torch.cuda.is_current_stream_capturing():
         return None
     best = None
+    nconc = TUNE_CONCURRENT[0]
+    side = [torch.cuda.Stream() for _ in range(nconc)] if nconc > 1 else []
+
+    def once(c):
+        if not side:
+            run(c)
+            return
+        main = torch.cuda.current_stream()
+        for st in side:  # the copies write the same outputs: identical values, timing only
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                run(c)
+        for st in side:
+            main.wait_stream(st)
+    log = TUNE_LOG.setdefault(key_str(key) + ("" if variant is None else "|" + str(variant)), {})
     for c in cands:
         if c in TILES_EXCLUDED:
             continue
         try:
-            run(c)
-            run(c)
+            once(c)
+            once(c)
             evs = []
             for _ in range(TUNE_REPS[0]):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                run(c)
+                once(c)
                 e1.record()
                 evs.append((e0, e1))
         except _lib.SmpqError:
@@ -583,6 +604,7 @@ def _choose_tile(key, run, cands, variant=None):
         torch.cuda.synchronize()
         ts = sorted(a.elapsed_time(b) for a, b in evs)
         t_med = ts[len(ts) // 2]
+        log[c] = round(t_med * 1e3, 2)
         if best is None or t_med < best[0]:
             best = (t_med, c)
     if best is None:

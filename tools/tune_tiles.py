@@ -45,12 +45,16 @@ def main():
     ap.add_argument("--reps", type=int, default=25)
     ap.add_argument("--out", default=None)
     ap.add_argument("--configs", default="r50_mixed:256,r18_u8:256,r34_4bit:512")
+    ap.add_argument("--concurrent", type=int, default=1,
+                    help="time each candidate as this many copies launched together on their own streams")
+    ap.add_argument("--log", default=None, help="write every candidate's median per key (us) to this JSON")
     args = ap.parse_args()
     __graft_entry__.build()
     import resnet
     from smpq import assignments, engine, ops
     ops.load_tile_table("off")
     ops.TUNE_REPS[0] = args.reps
+    ops.TUNE_CONCURRENT[0] = args.concurrent
     dev = torch.device("cuda", 0)
     for item in args.configs.split(","):
         name, batch = item.split(":")
@@ -72,8 +76,9 @@ def main():
            "device": torch.cuda.get_device_name(0),
            "arch": getattr(torch.cuda.get_device_properties(0), "gcnArchName", "gfx950"),
            "made": datetime.datetime.utcnow().strftime("%Y-%m-%d %H:%M UTC"),
-           "method": "tools/tune_tiles.py: median of %d timed launches per candidate (after 2 warm-ups), "
-                     "workloads %s" % (args.reps, args.configs),
+           "method": "tools/tune_tiles.py: median of %d timed launches per candidate (after 2 warm-ups)%s, "
+                     "workloads %s" % (args.reps, "" if args.concurrent == 1 else
+                                       ", each launch %d copies on their own streams" % args.concurrent, args.configs),
            "key": "tuned_conv2d_q: n|h|w|cin|cout|kh|kw|stride|pad|limbs|wlimbs|res_f32|emit_q|want_f32|res_q; "
                   "tuned_stem_conv_s2d: stem_s2d|planes|codes|h|w|y_absmax|emit_q|want_f32",
            "tiles": table_entries(ops)}
@@ -81,6 +86,9 @@ def main():
         json.dump(doc, f, indent=1, sort_keys=False)
         f.write("\n")
     print("wrote %s (%d tiles)" % (out, len(doc["tiles"])))
+    if args.log:
+        with open(args.log, "w") as f:
+            json.dump(ops.TUNE_LOG, f, indent=1)
 
 
 if __name__ == "__main__":
