@@ -31,6 +31,11 @@ SHAPES = [  # name, cin, cout, k, stride, hin, residual
     ("c1_2048_512_7", 2048, 512, 1, 1, 7, False),
     ("c3_256_1024_14", 256, 1024, 1, 1, 14, True),
     ("c1_1024_256_14", 1024, 256, 1, 1, 14, False),
+    ("c1_512_256_28", 512, 256, 1, 1, 28, False),
+    ("c1_512_128_28", 512, 128, 1, 1, 28, False),
+    ("c3_128_512_28", 128, 512, 1, 1, 28, True),
+    ("c1_1024_512_14", 1024, 512, 1, 1, 14, False),
+    ("c3_512_2048_7", 512, 2048, 1, 1, 7, True),
 ]
 dev = torch.device("cuda")
 for name, cin, cout, k, s, h, res in SHAPES:
@@ -54,7 +59,7 @@ for name, cin, cout, k, s, h, res in SHAPES:
     for c in ops.tile_configs():
         if not ops._tile_fits(c, L, 1, cout, cin, k) or (CFGS is not None and c not in CFGS):
             continue
-        kw = dict(emit_range=8.0, overflow=ovf, want_f32=False) if static else {}
+        kw = dict(emit_range=8.0, overflow=ovf, want_f32=False, relu=True) if static else {}
         if res:
             kw.update(residual_q=rq, residual_range=4.0) if static else kw.update(
                 residual=torch.zeros(B, ho, ho, cout, device=dev))
