@@ -39,7 +39,6 @@ struct ConvArgs {
   // the 64-B K slices of 16 consecutive output channels are one contiguous KiB, so every weight
   // DMA piece is whole cache lines instead of 16 half lines
   int w_kmajor;
-  int ntiles;  // tiles of a persistent-block launch (set by the tile launcher)
 };
 
 // Division by a runtime constant d >= 1 for numerators in [0, 2^31): p = 31 + ceil(log2 d),

@@ -5,9 +5,7 @@
 
 namespace smpq {
 
-#define SMPQ_GLDS_FAMILY(L, LW)                                                 \
-  extern template int launch_cfg<L, LW>(int, const ConvArgs&, hipStream_t); \
-  extern template int launch_pcfg<L, LW>(int, const ConvArgs&, hipStream_t);
+#define SMPQ_GLDS_FAMILY(L, LW) extern template int launch_cfg<L, LW>(int, const ConvArgs&, hipStream_t);
 SMPQ_GLDS_FAMILY(1, 1)
 SMPQ_GLDS_FAMILY(2, 1)
 SMPQ_GLDS_FAMILY(3, 1)
@@ -19,31 +17,16 @@ SMPQ_GLDS_FAMILY(3, 3)
 
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
-// C-ABI tile numbers: [0, kNumGlds) LDS-DMA tiles, then the halo tiles, then the persistent-block
-// tiles (kGldsP: a kGlds base tile whose blocks run several tiles each)
-int glds_num_cfgs() { return kNumGlds + halo_num_cfgs() + kNumGldsP; }
+int glds_num_cfgs() { return kNumGlds + halo_num_cfgs(); }
 
-// index into kGldsP, or -1
-static int persist_index(int cfg) {
-  const int p = cfg - kNumGlds - halo_num_cfgs();
-  return p >= 0 && p < kNumGldsP ? p : -1;
-}
+bool glds_is_halo(int cfg) { return cfg >= kNumGlds; }
 
-bool glds_is_halo(int cfg) { return cfg >= kNumGlds && persist_index(cfg) < 0; }
-
-// the kGlds entry a (plain or persistent) LDS-DMA tile runs
-static int glds_base(int cfg) {
-  const int p = persist_index(cfg);
-  return p >= 0 ? kGldsP[p].base : cfg;
-}
-
-int glds_cfg_bk(int cfg) { return glds_is_halo(cfg) ? 64 : kGlds[glds_base(cfg)].bk; }
+int glds_cfg_bk(int cfg) { return cfg >= kNumGlds ? 64 : kGlds[cfg].bk; }
 
 // Same rules as launch_one / launch_glds (accumulator budget, K-step width, LDS per CU).
 bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs) {
-  if (glds_is_halo(cfg)) return halo_supported(cfg - kNumGlds, cin, cout, kh, kw, limbs, wlimbs);
-  const bool per = persist_index(cfg) >= 0;
-  const GldsCfg& c = kGlds[glds_base(cfg)];
+  if (cfg >= kNumGlds) return halo_supported(cfg - kNumGlds, cin, cout, kh, kw, limbs, wlimbs);
+  const GldsCfg& c = kGlds[cfg];
   if (cin % 64 != 0 || cout % 16 != 0 || (c.bk == 128 && cin % 128 != 0)) return false;
   if (wlimbs == 3 && limbs != 3) return false;
   const int smin = limbs + wlimbs - 4 > 0 ? limbs + wlimbs - 4 : 0;
@@ -55,7 +38,7 @@ bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int w
   int lds = (nsteps < c.stages ? nsteps : c.stages) * stage;
   if (c.wc % 4 == 0) {  // worst case: staged output tile + residual tile (static-range epilogue)
     const int tile = limbs * bp * bc;
-    lds = per ? lds + 2 * tile : (lds > tile ? lds : tile) + tile;
+    lds = (lds > tile ? lds : tile) + tile;
   }
   return lds <= 160 * 1024;
 }
@@ -79,8 +62,8 @@ int glds_default_cfg(const ConvArgs& a, int limbs, int wlimbs) {
 }
 
 void glds_cfg_info(int cfg, int* bm, int* bn, int* threads) {
-  if (glds_is_halo(cfg)) return halo_cfg_info(cfg - kNumGlds, bm, bn, threads);
-  const GldsCfg& c = kGlds[glds_base(cfg)];
+  if (cfg >= kNumGlds) return halo_cfg_info(cfg - kNumGlds, bm, bn, threads);
+  const GldsCfg& c = kGlds[cfg];
   *bm = 16 * c.wp * c.wavesp;  // pixels (GEMM rows)
   *bn = 16 * c.wc * c.wavesc;  // channels
   *threads = 64 * c.wavesc * c.wavesp;
@@ -103,24 +86,7 @@ int launch_glds(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s
   if ((!a.s2d && a.cin % kKStep != 0) || a.cout % 16 != 0 || !glds_planes_ok(a, limbs, wlimbs))
     return fail(SMPQ_E_INVALID,
                 "smpq_conv2d_fwd: LDS-DMA tile configs need cin % 64 == 0, cout % 16 == 0 and planes < 2 GiB");
-  if (glds_is_halo(cfg)) return launch_halo(cfg - kNumGlds, limbs, wlimbs, a, s);
-  const int p = persist_index(cfg);
-  if (p >= 0) {
-    if (a.s2d) return fail(SMPQ_E_INVALID, "smpq_stem_conv_s2d_q: tile config not built for the stem");
-    if (wlimbs == 1) {
-      switch (limbs) {
-        case 1: return launch_pcfg<1, 1>(p, a, s);
-        case 2: return launch_pcfg<2, 1>(p, a, s);
-        default: return launch_pcfg<3, 1>(p, a, s);
-      }
-    }
-    if (wlimbs == 3) return launch_pcfg<3, 3>(p, a, s);
-    switch (limbs) {
-      case 1: return launch_pcfg<1, 2>(p, a, s);
-      case 2: return launch_pcfg<2, 2>(p, a, s);
-      default: return launch_pcfg<3, 2>(p, a, s);
-    }
-  }
+  if (cfg >= kNumGlds) return launch_halo(cfg - kNumGlds, limbs, wlimbs, a, s);
   if (a.s2d) {
     if (wlimbs == 2 && limbs == 1) return launch_s2d<1, 2>(cfg, a, s);
     if (wlimbs == 2 && limbs == 2) return launch_s2d<2, 2>(cfg, a, s);

@@ -5,5 +5,4 @@
 
 namespace smpq {
 template int launch_cfg<SMPQ_INST_L, SMPQ_INST_LW>(int, const ConvArgs&, hipStream_t);
-template int launch_pcfg<SMPQ_INST_L, SMPQ_INST_LW>(int, const ConvArgs&, hipStream_t);
 }  // namespace smpq

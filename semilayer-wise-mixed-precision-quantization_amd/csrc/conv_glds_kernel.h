@@ -36,10 +36,9 @@ namespace smpq {
 
 namespace {
 
-// Diagnostic builds only (tools/build_variant.py / ablate_build.sh compile separate libraries with -DSMPQ_DIAG_ABLATE=N;
+// Diagnostic builds only (tools/ablate_glds.sh compiles separate libraries with -DSMPQ_DIAG_ABLATE=N;
 // results are wrong with any bit set): 1 no residual loads, 2 no limb-plane stores, 4 no operand
-// DMA, 8 no MFMA, 16 no epilogue; 64 (results stay right) never stages the epilogue's limb-plane tiles
-// through LDS (residual and output move straight between registers and HBM).
+// DMA, 8 no MFMA, 16 no epilogue.
 #ifndef SMPQ_DIAG_ABLATE
 #define SMPQ_DIAG_ABLATE 0
 #endif
@@ -87,10 +86,9 @@ __device__ unsigned long long* smpq_stamps;
 // the offset sums and their correction compile away (a runtime-false branch still cost the
 // epilogue ~50 register moves per wave to merge the two paths' accumulators).
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
-          int LEAN = 0, bool PIPE = false, bool OFF = true, bool PER = false>
+          int LEAN = 0, bool PIPE = false, bool OFF = true>
 __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, int8_t* lds) {
   static_assert(BK == 64 || BK == 128, "BK");
-  static_assert(!PER || (!PIPE && !S2D), "persistent blocks: plain K loop, not the stem");
   static_assert(!S2D || BK == 64, "the s2d stem uses 64-B K steps");
   constexpr int NW = WAVES_C * WAVES_P;
   constexpr int BC = 16 * WC * WAVES_C;  // channels per block tile
@@ -127,19 +125,13 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   const int wc = wave / WAVES_P, wp = wave % WAVES_P;
 
   // ---- XCD-aware tile order ----------------------------------------------------------------
-  // PER (persistent blocks): `total` is the tile count, the grid a multiple of 8 blocks, and block
-  // b runs the tiles of virtual ids b, b + grid, b + 2 grid, ... (all of them on b's XCD)
   const int ntc = (a.cout + BC - 1) / BC;
   const int full = total & ~7;
-  auto origin = [&](int v, int& m0, int& n0) {
-    int t = v;
-    if (t < full) t = (t & 7) * (full >> 3) + (t >> 3);
-    const int tq = fast_div(t, a.ntc_mul, a.ntc_shr);  // t / ntc
-    m0 = tq * BP;
-    n0 = (t - tq * ntc) * BC;
-  };
-  int vt = bid, m0, n0;
-  origin(vt, m0, n0);
+  int t = bid;
+  if (t < full) t = (t & 7) * (full >> 3) + (t >> 3);
+  const int tq = fast_div(t, a.ntc_mul, a.ntc_shr);  // t / ntc
+  const int m0 = tq * BP;
+  const int n0 = (t - tq * ntc) * BC;
   const int hw_out = a.ho * a.wo;
 
   const v4i wrs = make_rsrc(a.codes, (long long)LW * a.wplane);
@@ -152,8 +144,6 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   const int prow = lane / CPR;
   auto pchunk_of = [&](int q) { return (lane % CPR) ^ swz<BK>((RPP * q + prow) & 15); };
   unsigned wsrc[WSLOTS];
-  int apix[ASLOTS], aih[ASLOTS], aiw[ASLOTS];
-  auto setup_src = [&](int m0, int n0) {  // this tile's per-lane DMA source offsets
 #pragma unroll
   for (int s = 0; s < WSLOTS; ++s) {
     const int p = wave + NW * s;  // weight piece: limb p / (BC/RPP), rows RPP * (p % (BC/RPP)) + ...
@@ -166,6 +156,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
                                       : (long long)row * a.K + 16 * lc;
     wsrc[s] = (p < WPIECES && row < a.cout) ? (unsigned)((long long)lw * a.wplane + woff) : kOOB;
   }
+  int apix[ASLOTS], aih[ASLOTS], aiw[ASLOTS];
 #pragma unroll
   for (int s = 0; s < ASLOTS; ++s) {
     const int p = wave + NW * s;  // activation piece: limb p / (BP/RPP), rows RPP * (p % (BP/RPP)) + ...
@@ -192,8 +183,6 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       apix[s] = 0;
     }
   }
-  };
-  setup_src(m0, n0);
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
 
   // K position of step ks: tap (kr, kc), channel chunk c0 (scalar, advanced incrementally)
@@ -226,60 +215,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       }
     }
   };
-  // fragment read offset inside a 16-row block of a [rows][BK] region, per MFMA K step h
-  const int frow = lane & 15;
-  int rd[KH];
-#pragma unroll
-  for (int h = 0; h < KH; ++h) rd[h] = frow * BK + 16 * ((4 * h + (lane >> 4)) ^ swz<BK>(frow));
-  const int nsteps = a.ksteps / KH;  // a.ksteps counts 64-wide K steps
 
-  // DMA pieces this wave issues per K step (wave-uniform): the counted vmcnt below. When the
-  // pieces divide evenly over the waves the count is a compile-time constant (PPW) and so are the
-  // steady-state waits.
-  constexpr bool kUniform = (WPIECES % NW) == 0 && (APIECES % NW) == 0;
-  constexpr int PPW = (WPIECES + APIECES) / NW;
-  int ppw = 0;
-#pragma unroll
-  for (int s = 0; s < WSLOTS; ++s) ppw += (wave + NW * s < WPIECES) ? 1 : 0;
-#pragma unroll
-  for (int s = 0; s < ASLOTS; ++s) ppw += (wave + NW * s < APIECES) ? 1 : 0;
-  if constexpr (kUniform) ppw = PPW;
-
-  int kr = 0, kc = 0, c0 = 0;  // K position of the next step to issue
-  auto advance = [&]() {
-    c0 += BK;
-    if (c0 == a.cin) {
-      c0 = 0;
-      if (++kc == a.kw) {
-        kc = 0;
-        ++kr;
-      }
-    }
-  };
-  int nissued = 0, wbuf = 0, rbuf = 0;
-  auto issue_next = [&]() {
-    if (nissued < nsteps) {
-      issue(wbuf, kr, kc, c0, nissued);
-      advance();
-      ++nissued;
-      wbuf = wbuf + 1 == NST ? 0 : wbuf + 1;
-    }
-  };
-  // wait until this wave's DMA of step `ready` has landed (younger steps may still fly)
-  auto wait_step = [&](int ready) {
-    const int d = nissued - ready - 1;  // steps issued after it
-    if (kUniform && d == NST - 1) {
-      wait_vm<PPW * (NST - 1)>();
-    } else if (kUniform && d == NST - 2) {
-      wait_vm<PPW * (NST - 2)>();
-    } else {
-      wait_vmcnt(d * ppw);
-    }
-  };
-  const int nst_eff = nsteps < NST ? nsteps : NST;
-  bool pre = false;  // (PER) this tile's first K steps were issued during the previous tile's epilogue
-
-  for (;;) {  // the block's tiles (one unless PER)
   v4i acc[NACC][WC][WP];
 #pragma unroll
   for (int s = 0; s < NACC; ++s)
@@ -293,6 +229,13 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   for (int l = 0; l < L; ++l)
 #pragma unroll
     for (int j = 0; j < WP; ++j) rs[l][j] = 0;
+
+  // fragment read offset inside a 16-row block of a [rows][BK] region, per MFMA K step h
+  const int frow = lane & 15;
+  int rd[KH];
+#pragma unroll
+  for (int h = 0; h < KH; ++h) rd[h] = frow * BK + 16 * ((4 * h + (lane >> 4)) ^ swz<BK>(frow));
+  const int nsteps = a.ksteps / KH;  // a.ksteps counts 64-wide K steps
 
   // Output coordinates of this lane: channels chan[i] + 0..3 of pixel mrow[j]; ooff = element
   // offset in an NHWC plane, or kOOB (then buffer loads read 0 and buffer stores are dropped).
@@ -321,7 +264,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
   // wave-instruction moves 64 contiguous bytes of 16 pixel rows straight from registers.
   constexpr bool TR = TRT;
   constexpr int NQ = TR ? WC / 4 : 1;
-  const bool lines = (kAblate & 64) ? false : (kAblate & 32) ? BC >= 128 : (BC >= 128 || BC == a.cout);
+  const bool lines = (kAblate & 32) ? BC >= 128 : (BC >= 128 || BC == a.cout);
   // limb-plane residual (compile-time in the LEAN 2 / 3 variants: no merged paths in the epilogue)
   const bool has_rq = LEAN == 3 || (LEAN != 2 && LEAN != 4 && a.res_q != nullptr);
   const bool stage_res = TR && has_rq && lines, stage_out = TR && a.yq && lines;
@@ -336,10 +279,8 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 
   // residual limb planes: issued now, consumed in the epilogue (latency hidden behind the K loop)
   int rq[WC][WP][L];
-  // LDS layout: operand stages, then (PER) the staged output tile, then the residual tile
-  const int outoff = PER ? nst_eff * STAGE : 0;
-  const int resoff = PER ? outoff + (stage_out ? TILEB : 0)
-                         : ((stage_out && TILEB > nst_eff * STAGE) ? TILEB : nst_eff * STAGE);
+  const int nst_eff = nsteps < NST ? nsteps : NST;
+  const int resoff = (stage_out && TILEB > nst_eff * STAGE) ? TILEB : nst_eff * STAGE;  // LDS layout
   if constexpr (TR) {
     if (has_rq && !stage_res) {
       const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.res_q), 0, (int)(L * oplane),
@@ -388,6 +329,30 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
                                                                                   (unsigned)((long long)l * oplane), 0);
   }
 
+  // DMA pieces this wave issues per K step (wave-uniform): the counted vmcnt below. When the
+  // pieces divide evenly over the waves the count is a compile-time constant (PPW) and so are the
+  // steady-state waits.
+  constexpr bool kUniform = (WPIECES % NW) == 0 && (APIECES % NW) == 0;
+  constexpr int PPW = (WPIECES + APIECES) / NW;
+  int ppw = 0;
+#pragma unroll
+  for (int s = 0; s < WSLOTS; ++s) ppw += (wave + NW * s < WPIECES) ? 1 : 0;
+#pragma unroll
+  for (int s = 0; s < ASLOTS; ++s) ppw += (wave + NW * s < APIECES) ? 1 : 0;
+  if constexpr (kUniform) ppw = PPW;
+
+  int kr = 0, kc = 0, c0 = 0;  // K position of the next step to issue
+  auto advance = [&]() {
+    c0 += BK;
+    if (c0 == a.cin) {
+      c0 = 0;
+      if (++kc == a.kw) {
+        kc = 0;
+        ++kr;
+      }
+    }
+  };
+  int nissued = 0, wbuf = 0, rbuf = 0;
   // fragments of one MFMA K step of a stage
   struct Frags {
     v4i w[LW][WC], a[L][WP];
@@ -430,6 +395,25 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
             acc[l + lw - SMIN][i][j] =
                 __builtin_amdgcn_mfma_i32_16x16x64_i8(f.w[lw][i], f.a[l][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
       }
+  };
+  auto issue_next = [&]() {
+    if (nissued < nsteps) {
+      issue(wbuf, kr, kc, c0, nissued);
+      advance();
+      ++nissued;
+      wbuf = wbuf + 1 == NST ? 0 : wbuf + 1;
+    }
+  };
+  // wait until this wave's DMA of step `ready` has landed (younger steps may still fly)
+  auto wait_step = [&](int ready) {
+    const int d = nissued - ready - 1;  // steps issued after it
+    if (kUniform && d == NST - 1) {
+      wait_vm<PPW * (NST - 1)>();
+    } else if (kUniform && d == NST - 2) {
+      wait_vm<PPW * (NST - 2)>();
+    } else {
+      wait_vmcnt(d * ppw);
+    }
   };
 
   if constexpr (PIPE) {
@@ -480,11 +464,9 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   } else {
-    if (!pre) {
 #pragma unroll
-      for (int st = 0; st < NST - 1; ++st)
-        if (st < nsteps) issue_next();
-    }
+    for (int st = 0; st < NST - 1; ++st)
+      if (st < nsteps) issue_next();
     SMPQ_STAMP(1);
     for (int ks = 0; ks < nsteps; ++ks) {
       // this wave's DMA of step ks has landed (the younger steps' may still fly) and its reads of
@@ -493,12 +475,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
       if constexpr (NST == 2) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       } else {
-        // (PER: the previous tile's stores are younger than this tile's first K steps, and a
-        // counted wait assumes in-order returns: wait for everything once per tile)
-        if (PER && ks == 0)
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else
-          wait_step(ks);
+        wait_step(ks);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
       __builtin_amdgcn_s_barrier();
@@ -535,23 +512,6 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     }
   }
 
-  // PER: the next tile's first K steps go out now, under this tile's epilogue
-  int m0n = 0, n0n = 0;
-  const int vn = vt + (int)gridDim.x;
-  const bool more = PER && vn < total;
-  if constexpr (PER) {
-    if (more) {
-      __syncthreads();  // every wave's fragment reads of this tile's stages are done
-      origin(vn, m0n, n0n);
-      setup_src(m0n, n0n);
-      kr = kc = c0 = 0;
-      nissued = wbuf = rbuf = 0;
-#pragma unroll
-      for (int st = 0; st < NST - 1; ++st)
-        if (st < nsteps) issue_next();
-      pre = true;
-    }
-  }
   SMPQ_STAMP(21);
   if constexpr ((kAblate & 16) != 0) {  // diagnostic: no epilogue at all (keep the MFMAs live)
     int keep = 0;
@@ -816,7 +776,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
 #pragma unroll
         for (int j = 0; j < WP; ++j)
 #pragma unroll
-          for (int l = 0; l < L; ++l) *reinterpret_cast<unsigned*>(lds + tile_word(outoff, i, j, l)) = wq[i][j][l];
+          for (int l = 0; l < L; ++l) *reinterpret_cast<unsigned*>(lds + tile_word(0, i, j, l)) = wq[i][j][l];
       __syncthreads();
       SMPQ_STAMP(27);
       constexpr int RCPR = BC / 16, ITEMS = TILEB / 16;
@@ -826,7 +786,7 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
         if (it < ITEMS) {
           const int l = it / (BP * RCPR), rem = it - l * (BP * RCPR);
           const int rt = rem / RCPR, c = rem - rt * RCPR;
-          const v4i v = *reinterpret_cast<const v4i*>(lds + outoff + l * BP * BC + rt * BC + 16 * (c ^ swze<BC>(rt & 15)));
+          const v4i v = *reinterpret_cast<const v4i*>(lds + l * BP * BC + rt * BC + 16 * (c ^ swze<BC>(rt & 15)));
           const bool ok = m0 + rt < a.M && n0 + 16 * c < a.cout;
           const unsigned off = ok ? (unsigned)((long long)(m0 + rt) * a.cout + n0 + 16 * c) : kOOB;
           if (!(kAblate & 2) || v.x == 0x12345679)
@@ -857,24 +817,13 @@ __device__ __forceinline__ void qconv_glds_body(ConvArgs a, int bid, int total, 
     stamp_base[23] = ((unsigned long long)(xcc & 0xf) << 16) | ((id >> 8) & 0xff);
   }
 #endif
-  if constexpr (!PER) {
-    break;
-  } else {
-    if (!more) break;
-    vt = vn;
-    m0 = m0n;
-    n0 = n0n;
-    __syncthreads();  // the epilogue's LDS tiles (residual, staged output) are free again
-  }
-  }  // tiles
 }
 
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, int MINW, bool S2D, int NST, int BK,
-          int LEAN = 0, bool PIPE = false, bool OFF = true, bool PER = false>
+          int LEAN = 0, bool PIPE = false, bool OFF = true>
 __global__ __launch_bounds__(64 * WAVES_C * WAVES_P, MINW) void qconv_glds_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // min(NST, ksteps) stages
-  qconv_glds_body<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, LEAN, PIPE, OFF, PER>(
-      a, blockIdx.x, PER ? a.ntiles : (int)gridDim.x, lds);
+  qconv_glds_body<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, LEAN, PIPE, OFF>(a, blockIdx.x, gridDim.x, lds);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -929,10 +878,9 @@ constexpr GldsCfg kGlds[] = {
     {1, 4, 4, 1, 4, 64, 1},   // 35: as 24
     {2, 2, 2, 2, 3, 128, 1},  // 36: as 26
 };
-// PER: persistent blocks, `tpb` tiles per block (0: as many blocks as fit the GPU at once)
 template <int L, int LW, int WAVES_C, int WAVES_P, int WC, int WP, bool S2D = false, int NST = 2, int MINW = 2,
-          int BK = 64, bool PIPE = false, bool PER = false>
-static int launch_one(const ConvArgs& a, hipStream_t stream, int tpb = 0) {
+          int BK = 64, bool PIPE = false>
+static int launch_one(const ConvArgs& a, hipStream_t stream) {
   constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
   if constexpr ((L + LW - 1 - SMIN) * WC * WP * 4 > 128) {
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: tile config too large for these limb counts");
@@ -950,16 +898,12 @@ static int launch_one(const ConvArgs& a, hipStream_t stream, int tpb = 0) {
     // operand stages, enlarged to hold the staged output tile, + the residual tile (kernel layout)
     constexpr bool TRT = (WC % 4) == 0;
     constexpr int TILEB = L * BP * BC;
-    const bool lines = !(kAblate & 64) && (BC >= 128 || BC == a.cout);
+    const bool lines = BC >= 128 || BC == a.cout;
     int lds_bytes = (nsteps < NST ? nsteps : NST) * STAGE;
-    if (PER) {  // the staged output tile has its own region (the next tile's DMA fills the stages)
-      if (TRT && lines && a.yq) lds_bytes += TILEB;
-    } else if (TRT && lines && a.yq && TILEB > lds_bytes) {
-      lds_bytes = TILEB;
-    }
+    if (TRT && lines && a.yq && TILEB > lds_bytes) lds_bytes = TILEB;
     if (TRT && lines && a.res_q) lds_bytes += TILEB;
     if (lds_bytes > kMaxLds) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: tile config needs more LDS than a CU has");
-    constexpr int kMaxNeed = PER ? NST * STAGE + 2 * TILEB : (NST * STAGE > TILEB ? NST * STAGE : TILEB) + TILEB;
+    constexpr int kMaxNeed = (NST * STAGE > TILEB ? NST * STAGE : TILEB) + TILEB;
     ConvArgs b = a;
     fast_div_init((int)nt, b.ntc_mul, b.ntc_shr);
     const bool lean = L >= 2 && a.yq && !a.y && !a.residual && !a.y_absmax;
@@ -968,16 +912,16 @@ static int launch_one(const ConvArgs& a, hipStream_t stream, int tpb = 0) {
     // residual variants too: the block convs of the quantized ResNets)
     constexpr bool kV = LW == 1 && L >= 2;
     constexpr int kLean = L >= 2 ? 1 : 0;
-    auto k00 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, 0, PIPE, false, PER>;
-    auto k10 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kLean, PIPE, false, PER>;
-    auto k20 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 2 : kLean, PIPE, false, PER>;
-    auto k30 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 3 : kLean, PIPE, false, PER>;
-    auto k40 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, L >= 2 ? 4 : 0, PIPE, false, PER>;
-    auto k01 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, 0, PIPE, LW == 1, PER>;
-    auto k11 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kLean, PIPE, LW == 1, PER>;
-    auto k21 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 2 : kLean, PIPE, LW == 1, PER>;
-    auto k31 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 3 : kLean, PIPE, LW == 1, PER>;
-    auto k41 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, L >= 2 ? 4 : 0, PIPE, LW == 1, PER>;
+    auto k00 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, 0, PIPE, false>;
+    auto k10 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kLean, PIPE, false>;
+    auto k20 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 2 : kLean, PIPE, false>;
+    auto k30 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 3 : kLean, PIPE, false>;
+    auto k40 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, L >= 2 ? 4 : 0, PIPE, false>;
+    auto k01 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, 0, PIPE, LW == 1>;
+    auto k11 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kLean, PIPE, LW == 1>;
+    auto k21 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 2 : kLean, PIPE, LW == 1>;
+    auto k31 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, kV ? 3 : kLean, PIPE, LW == 1>;
+    auto k41 = qconv_glds_kernel<L, LW, WAVES_C, WAVES_P, WC, WP, MINW, S2D, NST, BK, L >= 2 ? 4 : 0, PIPE, LW == 1>;
     auto set_lds = [](const void* k) {
       const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                kMaxNeed < kMaxLds ? kMaxNeed : kMaxLds);
@@ -1000,59 +944,8 @@ static int launch_one(const ConvArgs& a, hipStream_t stream, int tpb = 0) {
                                            : 1;
     const int vi = ev + ((LW == 1 && a.has_offset) ? 5 : 0);
     if (attrs[vi] != hipSuccess) return check_hip(attrs[vi], "qconv_glds_kernel LDS attribute");
-    long grid = mt * nt;
-    if constexpr (PER) {
-      b.ntiles = (int)(mt * nt);
-      long g;
-      if (tpb > 0) {
-        g = (grid + tpb - 1) / tpb;
-      } else {
-        static int cus = 0;
-        if (cus == 0) {
-          int dev = 0, n = 0;
-          if (hipGetDevice(&dev) == hipSuccess &&
-              hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-            cus = n;
-          else
-            (void)hipGetLastError();
-        }
-        int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(fns[vi]),
-                                                         64 * WAVES_C * WAVES_P, (size_t)lds_bytes) != hipSuccess) {
-          (void)hipGetLastError();
-          occ = 1;
-        }
-        g = (long)(cus > 0 ? cus : 256) * (occ > 0 ? occ : 1);
-      }
-      g = (g + 7) / 8 * 8;  // every block's tiles on its own XCD (block b -> XCD b % 8)
-      if (g < grid) grid = g;
-    }
-    hipLaunchKernelGGL(fns[vi], dim3((unsigned)grid), dim3(64 * WAVES_C * WAVES_P), lds_bytes, stream, b);
+    hipLaunchKernelGGL(fns[vi], dim3((unsigned)(mt * nt)), dim3(64 * WAVES_C * WAVES_P), lds_bytes, stream, b);
     return check_hip(hipGetLastError(), "qconv_glds_kernel launch");
-  }
-}
-
-// Persistent-block tile configurations (C-ABI numbers after the halo tiles): a base tile of kGlds
-// whose blocks loop over several tiles, issuing the next tile's first K steps before this tile's
-// epilogue (the short-K 1x1 convs spend a block's life in the first DMA wait and the epilogue).
-struct GldsPCfg {
-  int base, tpb;  // kGlds index; tiles per block (0: one wave of blocks over the whole GPU)
-};
-constexpr GldsPCfg kGldsP[] = {{9, 0}, {9, 2}, {2, 0}, {2, 2}, {18, 2}, {19, 2}, {3, 2}, {12, 2}};
-constexpr int kNumGldsP = sizeof(kGldsP) / sizeof(kGldsP[0]);
-
-template <int L, int LW>
-int launch_pcfg(int p, const ConvArgs& a, hipStream_t s) {
-  if (p < 0 || p >= kNumGldsP) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
-  const int tpb = kGldsP[p].tpb;
-  switch (kGldsP[p].base) {
-    case 2: return launch_one<L, LW, 2, 2, 4, 2, false, 2, 2, 64, false, true>(a, s, tpb);
-    case 3: return launch_one<L, LW, 1, 4, 4, 1, false, 2, 2, 64, false, true>(a, s, tpb);
-    case 9: return launch_one<L, LW, 2, 2, 4, 1, false, 2, 2, 64, false, true>(a, s, tpb);
-    case 12: return launch_one<L, LW, 2, 2, 4, 2, false, 3, 2, 64, false, true>(a, s, tpb);
-    case 18: return launch_one<L, LW, 2, 2, 4, 2, false, 2, 2, 128, false, true>(a, s, tpb);
-    case 19: return launch_one<L, LW, 2, 2, 4, 1, false, 2, 2, 128, false, true>(a, s, tpb);
-    default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad tile config");
   }
 }
 
