@@ -233,6 +233,8 @@ _STREAMS = {}
 
 # measurement (bench.py): run the batch slices one after another on the current stream
 SERIAL_SLICES = [False]
+# diagnostics: images of the first of two batch slices (0: an even split)
+SLICE_FIRST = [int(_os.environ.get("SMPQ_SLICE_FIRST", "0"))]
 # diagnostics: the first batch slice's stream at high priority (the others at normal priority)
 SLICE_PRIORITY = [_os.environ.get("SMPQ_SLICE_PRIORITY", "0") != "0"]
 
@@ -380,14 +382,19 @@ def _blocks(model):
     return [b for layer in (model.layer1, model.layer2, model.layer3, model.layer4) for b in layer]
 
 
-def _head(model, feat):
+def _head(model, feat, out=None):
     """avgpool + flatten + fc (resnet.py:216-218) on the last block's NHWC fp32 output: the
-    batch-invariant HIP kernel for the reference's modules, torch for anything else."""
+    batch-invariant HIP kernel for the reference's modules, torch for anything else. ``out``: the
+    rows of the batch's logits this slice fills (None: a new tensor)."""
     ap = model.avgpool
     if isinstance(model.fc, torch.nn.Linear) and isinstance(ap, torch.nn.AdaptiveAvgPool2d) \
             and ap.output_size in (1, (1, 1)) and feat.is_cuda and feat.shape[-1] % 4 == 0:
-        return ops.avgpool_fc(feat, model.fc.weight, model.fc.bias)
-    return model.fc(feat.mean(dim=(1, 2)))
+        return ops.avgpool_fc(feat, model.fc.weight, model.fc.bias, out=out)
+    y = model.fc(feat.mean(dim=(1, 2)))
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
 
 
 def _features(model, x, ctx):
@@ -411,6 +418,8 @@ def _forward(model, x, ctx):
         if len(parts) == 1:
             step = (n + nst - 1) // nst
             parts = [(s, min(n, s + step)) for s in range(0, n, step)]
+            if nst == 2 and 0 < SLICE_FIRST[0] < n:
+                parts = [(0, SLICE_FIRST[0]), (SLICE_FIRST[0], n)]
         main = torch.cuda.current_stream()
         for s0, s1 in parts:  # shared per-layer range tensors exist before the fork
             ctx.n = s1 - s0
@@ -419,6 +428,10 @@ def _forward(model, x, ctx):
                     ctx.range_tensor(m)
         logits = []
         lanes = min(nst, len(parts))
+        # every slice writes its rows of the batch's logits (allocated before the fork: no
+        # concatenation after the join)
+        y = torch.empty(n, model.fc.out_features, dtype=torch.float32, device=x.device) \
+            if isinstance(model.fc, torch.nn.Linear) else None
         for i in range(lanes):
             _stream((x.device, "slice", i)).wait_stream(main)
         for i, (s0, s1) in enumerate(parts):
@@ -426,10 +439,12 @@ def _forward(model, x, ctx):
             # another on the current stream, so that per-launch events time each kernel alone
             with torch.cuda.stream(main if SERIAL_SLICES[0] else _stream((x.device, "slice", i % lanes))):
                 ctx.n, ctx.lane = s1 - s0, i % lanes
-                logits.append(_head(model, _features(model, x[s0:s1], ctx)))
+                logits.append(_head(model, _features(model, x[s0:s1], ctx), out=None if y is None else y[s0:s1]))
         for i in range(lanes):
             main.wait_stream(_stream((x.device, "slice", i)))
         ctx.n, ctx.lane = n, None
+        if y is not None:
+            return y
         return torch.cat(logits) if len(logits) > 1 else logits[0]
     if len(parts) == 1:
         return _head(model, _features(model, x, ctx))
@@ -657,8 +672,15 @@ def _capture_locked(model, x_in, cal):
     torch.cuda.synchronize()
     with torch.cuda.graph(g, pool=pool[1]):
         ctx.overflow = torch.zeros(2, dtype=torch.int32, device=x_in.device)
+        # the weights' content check reads only the weights and writes only overflow[1]: it runs
+        # on a stream of its own beside the forward, off the step's critical path
+        main = torch.cuda.current_stream()
+        chk = _stream((x_in.device, "check"))
+        chk.wait_stream(main)
+        with torch.cuda.stream(chk):
+            cal[3].check(ctx.overflow[1:])
         y_static = _forward(model, x_in, ctx)
-        cal[3].check(ctx.overflow[1:])
+        main.wait_stream(chk)
     stats["graph_captures"] += 1
     return g, ctx, y_static
 

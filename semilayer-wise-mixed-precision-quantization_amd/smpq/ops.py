@@ -735,10 +735,12 @@ def kl_rows(p_ref, p, stats):
                                             _lib.stream_ptr()), "smpq_kl_rows")
 
 
-def avgpool_fc(x_nhwc, weight, bias):
+def avgpool_fc(x_nhwc, weight, bias, out=None):
     """AdaptiveAvgPool2d(1) + flatten + Linear (resnet.py:216-218) on the last block's NHWC fp32
-    output [n, h, w, c] -> logits [n, nout] fp32. Each logit is summed in an order fixed by c alone
-    (smpq_avgpool_fc), so an image's logits are the same bits in any batch or data-parallel shard."""
+    output [n, h, w, c] -> logits [n, nout] fp32 (into ``out`` when given: a contiguous [n, nout]
+    fp32 tensor, e.g. a batch slice's rows of the whole batch's logits). Each logit is summed in an
+    order fixed by c alone (smpq_avgpool_fc), so an image's logits are the same bits in any batch
+    or data-parallel shard."""
     _req(x_nhwc.is_cuda and x_nhwc.dtype == torch.float32 and x_nhwc.dim() == 4 and x_nhwc.is_contiguous(),
          "avgpool_fc: need contiguous NHWC fp32 on the GPU")
     n, h, w, c = x_nhwc.shape
@@ -749,7 +751,10 @@ def avgpool_fc(x_nhwc, weight, bias):
     b = None if bias is None else bias.detach().float().contiguous()
     _req(b is None or (b.numel() == nout and b.device == x_nhwc.device), "avgpool_fc: bias")
     pooled = torch.empty(n, c, dtype=torch.float32, device=x_nhwc.device)
-    out = torch.empty(n, nout, dtype=torch.float32, device=x_nhwc.device)
+    if out is None:
+        out = torch.empty(n, nout, dtype=torch.float32, device=x_nhwc.device)
+    _req(out.shape == (n, nout) and out.dtype == torch.float32 and out.is_contiguous() and out.device == x_nhwc.device,
+         "avgpool_fc: out must be a contiguous [n, nout] fp32 tensor on the input's device")
     with torch.cuda.device(x_nhwc.device):
         _lib.check(_lib.load().smpq_avgpool_fc(_lib.ptr(x_nhwc), n, h * w, c, _lib.ptr(wt), _lib.ptr(b), nout,
                                                _lib.ptr(pooled), _lib.ptr(out), _lib.stream_ptr()),
