@@ -233,8 +233,6 @@ _STREAMS = {}
 
 # measurement (bench.py): run the batch slices one after another on the current stream
 SERIAL_SLICES = [False]
-# diagnostics: images of the first of two batch slices (0: an even split)
-SLICE_FIRST = [int(_os.environ.get("SMPQ_SLICE_FIRST", "0"))]
 # diagnostics: the first batch slice's stream at high priority (the others at normal priority)
 SLICE_PRIORITY = [_os.environ.get("SMPQ_SLICE_PRIORITY", "0") != "0"]
 
@@ -418,8 +416,6 @@ def _forward(model, x, ctx):
         if len(parts) == 1:
             step = (n + nst - 1) // nst
             parts = [(s, min(n, s + step)) for s in range(0, n, step)]
-            if nst == 2 and 0 < SLICE_FIRST[0] < n:
-                parts = [(0, SLICE_FIRST[0]), (SLICE_FIRST[0], n)]
         main = torch.cuda.current_stream()
         for s0, s1 in parts:  # shared per-layer range tensors exist before the fork
             ctx.n = s1 - s0
