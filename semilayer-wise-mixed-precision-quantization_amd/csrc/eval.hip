@@ -156,8 +156,10 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const float* __restrict__ 
 // but c, so a row's logits are the same bits in any batch. Block: 8 images x 64 outputs; its 512
 // threads are 4 K-quarter groups of 128 (group g = threads 128 g ..), thread (i = t / 16, o4 = t % 16)
 // of a group owns outputs 4 o4 .. 4 o4 + 3 of image i over the group's quarter. Each group stages
-// its own 32-k chunks in LDS (k-major), the next chunk's global loads in flight under the current
-// chunk's FMAs; the groups' partials meet in LDS and group 0 adds them in quarter order.
+// its own 32-k chunks in LDS (k-major, two buffers), with the global loads of the next TWO chunks in
+// flight (two register sets) under the current chunk's FMAs — with one in flight the kernel waited
+// on each chunk's load latency in turn; the groups' partials meet in LDS and group 0 adds them in
+// quarter order.
 // (Round 4's one-chain kernel ran 16 x 64 tiles over all of k per thread: 110-190 us per R50 slice
 // of 128 images, a fifth of the chip busy; this one splits the chain four ways over 4x the blocks.)
 constexpr int kFcI = 8, kFcO = 64, kFcK = 32, kFcG = 4;
@@ -165,9 +167,10 @@ constexpr int kFcKQ = kFcK / 4;  // float4 per staged row
 __global__ __launch_bounds__(512) void fc_kernel(const float* __restrict__ pooled, int n, int c,
                                                  const float* __restrict__ w, const float* __restrict__ b, int nout,
                                                  float* __restrict__ logits) {
-  // per group, k-major LDS images (rows padded: the transposing writes stay at <= 4-way conflicts)
-  __shared__ __attribute__((aligned(16))) float sp[kFcG][kFcK][kFcI + 4];
-  __shared__ __attribute__((aligned(16))) float sw[kFcG][kFcK][kFcO + 4];
+  // per buffer and group, k-major LDS images (rows padded: the transposing writes stay at <= 4-way
+  // conflicts)
+  __shared__ __attribute__((aligned(16))) float sp[2][kFcG][kFcK][kFcI + 4];
+  __shared__ __attribute__((aligned(16))) float sw[2][kFcG][kFcK][kFcO + 4];
   __shared__ __attribute__((aligned(16))) float part[kFcG - 1][kFcI][kFcO];
   const int grp = threadIdx.x >> 7, tid = threadIdx.x & 127;
   const int i0 = blockIdx.y * kFcI, o0 = blockIdx.x * kFcO;
@@ -179,56 +182,68 @@ __global__ __launch_bounds__(512) void fc_kernel(const float* __restrict__ poole
   // staging: pooled kFcI images x kFcK k (one float4 per thread of the group's first kFcI * kFcKQ);
   // weights kFcO x kFcK k (kFcO * kFcKQ / 128 float4 per thread)
   constexpr int kWR = kFcO * kFcKQ / 128;
-  float4 vp, vw[kWR];
-  auto load = [&](int k0) {
+  struct Regs {
+    float4 p, w[kWR];
+  };
+  auto load = [&](Regs& r, int k0) {
     {
       const int ii = tid / kFcKQ, kq = tid % kFcKQ, img = i0 + ii, k = k0 + 4 * kq;
-      vp = (tid < kFcI * kFcKQ && img < n && k < ke) ? *reinterpret_cast<const float4*>(pooled + (long long)img * c + k)
-                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      r.p = (tid < kFcI * kFcKQ && img < n && k < ke) ? *reinterpret_cast<const float4*>(pooled + (long long)img * c + k)
+                                                      : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int r = 0; r < kWR; ++r) {
-      const int e = tid + 128 * r, oo = e / kFcKQ, kq = e % kFcKQ, o = o0 + oo, k = k0 + 4 * kq;
-      vw[r] = (o < nout && k < ke) ? *reinterpret_cast<const float4*>(w + (long long)o * c + k)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = 0; q < kWR; ++q) {
+      const int e = tid + 128 * q, oo = e / kFcKQ, kq = e % kFcKQ, o = o0 + oo, k = k0 + 4 * kq;
+      r.w[q] = (o < nout && k < ke) ? *reinterpret_cast<const float4*>(w + (long long)o * c + k)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  auto store = [&]() {
+  auto store = [&](const Regs& r, int buf) {
     if (tid < kFcI * kFcKQ) {
       const int ii = tid / kFcKQ, kq = tid % kFcKQ;
-      sp[grp][4 * kq][ii] = vp.x;
-      sp[grp][4 * kq + 1][ii] = vp.y;
-      sp[grp][4 * kq + 2][ii] = vp.z;
-      sp[grp][4 * kq + 3][ii] = vp.w;
+      sp[buf][grp][4 * kq][ii] = r.p.x;
+      sp[buf][grp][4 * kq + 1][ii] = r.p.y;
+      sp[buf][grp][4 * kq + 2][ii] = r.p.z;
+      sp[buf][grp][4 * kq + 3][ii] = r.p.w;
     }
 #pragma unroll
-    for (int r = 0; r < kWR; ++r) {
-      const int e = tid + 128 * r, oo = e / kFcKQ, kq = e % kFcKQ;
-      sw[grp][4 * kq][oo] = vw[r].x;
-      sw[grp][4 * kq + 1][oo] = vw[r].y;
-      sw[grp][4 * kq + 2][oo] = vw[r].z;
-      sw[grp][4 * kq + 3][oo] = vw[r].w;
+    for (int q = 0; q < kWR; ++q) {
+      const int e = tid + 128 * q, oo = e / kFcKQ, kq = e % kFcKQ;
+      sw[buf][grp][4 * kq][oo] = r.w[q].x;
+      sw[buf][grp][4 * kq + 1][oo] = r.w[q].y;
+      sw[buf][grp][4 * kq + 2][oo] = r.w[q].z;
+      sw[buf][grp][4 * kq + 3][oo] = r.w[q].w;
     }
   };
-  // every group runs the same number of chunk steps (barriers are block-wide); a group past its
-  // range computes nothing
-  const int steps = (cq + kFcK - 1) / kFcK;
-  load(kb);
-  for (int s = 0; s < steps; ++s) {
-    const int k0 = kb + s * kFcK;
-    store();
-    __syncthreads();
-    if (s + 1 < steps) load(k0 + kFcK);  // in flight under this chunk's FMAs
+  auto compute = [&](int buf, int k0) {
     const int kn = max(0, min(kFcK, ke - k0));
     for (int kk = 0; kk < kn; ++kk) {
-      const float pv = sp[grp][kk][ti];
-      const float4 wv = *reinterpret_cast<const float4*>(&sw[grp][kk][4 * to]);
+      const float pv = sp[buf][grp][kk][ti];
+      const float4 wv = *reinterpret_cast<const float4*>(&sw[buf][grp][kk][4 * to]);
       acc[0] = __fmaf_rn(pv, wv.x, acc[0]);
       acc[1] = __fmaf_rn(pv, wv.y, acc[1]);
       acc[2] = __fmaf_rn(pv, wv.z, acc[2]);
       acc[3] = __fmaf_rn(pv, wv.w, acc[3]);
     }
+  };
+  // every group runs the same number of chunk steps (barriers are block-wide); a group past its
+  // range computes nothing. Chunk s: register set / LDS buffer s % 2; the one barrier per chunk
+  // also certifies that every wave finished computing chunk s - 1, whose buffer chunk s + 1 refills.
+  const int steps = (cq + kFcK - 1) / kFcK;
+  Regs ra, rb;
+  load(ra, kb);
+  if (steps > 1) load(rb, kb + kFcK);
+  for (int s = 0; s < steps; s += 2) {
+    store(ra, 0);
     __syncthreads();
+    if (s + 2 < steps) load(ra, kb + (s + 2) * kFcK);
+    compute(0, kb + s * kFcK);
+    if (s + 1 < steps) {
+      store(rb, 1);
+      __syncthreads();
+      if (s + 3 < steps) load(rb, kb + (s + 3) * kFcK);
+      compute(1, kb + (s + 1) * kFcK);
+    }
   }
   if (grp > 0) {
 #pragma unroll
