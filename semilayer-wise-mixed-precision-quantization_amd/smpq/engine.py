@@ -163,6 +163,9 @@ class Ctx:
         self.overflow = torch.zeros(2, dtype=torch.int32, device=device) if ranges else None
         self._rt = cache if cache is not None else {}
         self.lane = None                # batch slice being enqueued (its own streams)
+        # (graph capture) the weights' content check, enqueued by _forward on the last batch
+        # slice's stream ahead of its work, or by the caller after the forward
+        self.pending_check = None
 
     def range_tensor(self, conv):
         key = (id(conv), self.n)
@@ -430,6 +433,14 @@ def _forward(model, x, ctx):
             if isinstance(model.fc, torch.nn.Linear) else None
         for i in range(lanes):
             _stream((x.device, "slice", i)).wait_stream(main)
+        if ctx.pending_check is not None and not SERIAL_SLICES[0] and lanes > 1:
+            # the content check reads only the weights and writes only overflow[1]: it goes ahead
+            # of the last slice's work (that slice starts while the first one's stem fills the
+            # GPU), off the step's critical path. (A stream forked only for it crashed graph
+            # replays on ROCm 7.2 beside the downsample forks.)
+            with torch.cuda.stream(_stream((x.device, "slice", lanes - 1))):
+                ctx.pending_check()
+            ctx.pending_check = None
         for i, (s0, s1) in enumerate(parts):
             # SERIAL_SLICES (bench.py's roofline region): the same slices and launches, one after
             # another on the current stream, so that per-launch events time each kernel alone
@@ -668,15 +679,11 @@ def _capture_locked(model, x_in, cal):
     torch.cuda.synchronize()
     with torch.cuda.graph(g, pool=pool[1]):
         ctx.overflow = torch.zeros(2, dtype=torch.int32, device=x_in.device)
-        # the weights' content check reads only the weights and writes only overflow[1]: it runs
-        # on a stream of its own beside the forward, off the step's critical path
-        main = torch.cuda.current_stream()
-        chk = _stream((x_in.device, "check"))
-        chk.wait_stream(main)
-        with torch.cuda.stream(chk):
-            cal[3].check(ctx.overflow[1:])
+        ctx.pending_check = lambda: cal[3].check(ctx.overflow[1:])
         y_static = _forward(model, x_in, ctx)
-        main.wait_stream(chk)
+        if ctx.pending_check is not None:  # (not enqueued inside a batch slice)
+            ctx.pending_check()
+            ctx.pending_check = None
     stats["graph_captures"] += 1
     return g, ctx, y_static
 
