@@ -433,20 +433,20 @@ def _forward(model, x, ctx):
             if isinstance(model.fc, torch.nn.Linear) else None
         for i in range(lanes):
             _stream((x.device, "slice", i)).wait_stream(main)
-        if ctx.pending_check is not None and not SERIAL_SLICES[0] and lanes > 1:
-            # the content check reads only the weights and writes only overflow[1]: it goes ahead
-            # of the last slice's work (that slice starts while the first one's stem fills the
-            # GPU), off the step's critical path. (A stream forked only for it crashed graph
-            # replays on ROCm 7.2 beside the downsample forks.)
-            with torch.cuda.stream(_stream((x.device, "slice", lanes - 1))):
-                ctx.pending_check()
-            ctx.pending_check = None
         for i, (s0, s1) in enumerate(parts):
             # SERIAL_SLICES (bench.py's roofline region): the same slices and launches, one after
             # another on the current stream, so that per-launch events time each kernel alone
             with torch.cuda.stream(main if SERIAL_SLICES[0] else _stream((x.device, "slice", i % lanes))):
                 ctx.n, ctx.lane = s1 - s0, i % lanes
                 logits.append(_head(model, _features(model, x[s0:s1], ctx), out=None if y is None else y[s0:s1]))
+                if i == 0 and lanes > 1 and ctx.pending_check is not None and not SERIAL_SLICES[0]:
+                    # the weights' content check (reads only the weights, writes only overflow[1])
+                    # after the first slice, which ends while the last one runs its narrow layer-4
+                    # convs: off the step's critical path. (Ahead of the last slice's work it
+                    # delayed that slice, -0.5 %; a stream forked only for it crashed a graph
+                    # replay beside the downsample forks on ROCm 7.2.)
+                    ctx.pending_check()
+                    ctx.pending_check = None
         for i in range(lanes):
             main.wait_stream(_stream((x.device, "slice", i)))
         ctx.n, ctx.lane = n, None
