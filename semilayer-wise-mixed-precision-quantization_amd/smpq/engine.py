@@ -760,14 +760,34 @@ def forward_fused(model, x):
     fresh = model.__dict__.pop("_smpq_recal", False)
     if _DP[0] is not None:
         # collective decision: every rank calibrates, or none does; and if any rank starts a new
-        # evaluation, all of them calibrate afresh (the same widening rule on every rank)
-        flags = torch.tensor([0 if (cal is not None and cal[1] == _signature(model)) else 1, int(fresh)],
-                             dtype=torch.int32, device=x.device)
-        need, fresh_any = _dp_max_(flags).tolist()
+        # evaluation, all of them calibrate afresh (the same widening rule on every rank). One MAX
+        # all-reduce and one host sync per forward carry all four flags — [overflow, stale, this
+        # rank needs a calibration, this rank starts a new evaluation] — after the forward, which
+        # runs optimistically (its result is dropped when any rank calibrates); as on one GPU,
+        # the graph replay is enqueued before the host's signature walk.
+        y = ovf = None
+        need_local = True
+        if cal is not None and not fresh:
+            if USE_GRAPH[0] and _graph_ready(model, x, cal):
+                y, ovf = _graph_forward(model, x, cal)
+                need_local = _signature(model) != cal[1]
+            elif cal[1] == _signature(model):
+                need_local = False
+                y, ovf = _graph_forward(model, x, cal) if USE_GRAPH[0] else _static_eager(model, x, cal)
+        flags = torch.zeros(4, dtype=torch.int32, device=x.device)
+        if ovf is not None:
+            flags[:2].copy_(ovf)
+        if need_local:
+            flags[2] = 1
+        if fresh:
+            flags[3] = 1
+        overflow, stale, need, fresh_any = _dp_max_(flags).tolist()
         if need or fresh_any:
             return calibrate(model, x, fresh=bool(fresh_any))
-        y, ovf = _graph_forward(model, x, cal) if USE_GRAPH[0] else _static_eager(model, x, cal)
-        _dp_max_(ovf)
+        if not overflow and not stale:
+            return y
+        stats["stale_reruns" if stale else "overflow_reruns"] += 1
+        return calibrate(model, x, stale=bool(stale))
     else:
         if cal is None or fresh:
             return calibrate(model, x, fresh=fresh)
