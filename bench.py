@@ -163,9 +163,25 @@ def attach_traffic(roof, config, limbs, batch, streams):
     roof["traffic_source"] = "profiles/" + os.path.basename(path) + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
 
 
-def cpu_baseline(arch, assign_name, budget_s=12.0):
-    """The reference CPU path (fp32 torch forward on the fake-quantized weights) on host cores."""
-    import numpy as np
+def _cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), or the platform's processor string."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(arch, assign_name, batch, iters=2):
+    """the reference CPU path (the fp32 torch forward of oracle/torch_ref.py, the
+    reference's own operators, on the weights fake-quantized by the oracle quantizer — bit-exact
+    with functions.channel_wise_quantizationperchan) at the config's batch: 1 warm-up and ``iters``
+    timed iterations of one [batch, 3, 224, 224] N(0,1) batch (seed 1), all of torch's CPU threads
+    (OMP_NUM_THREADS: the box's CPU share), the host CPU model recorded."""
     from oracle import quant_ref, torch_ref
     import resnet
     from smpq import assignments
@@ -178,20 +194,26 @@ def cpu_baseline(arch, assign_name, budget_s=12.0):
         key = names[id(assignments.conv_for_lnum(net, int(ln)))] + ".weight"
         sd[key][cn] = torch.from_numpy(quant_ref.apply_chain(sd[key][cn].numpy(), [int(b) for b in ch if b]))
     threads = torch.get_num_threads()
-    bs = 16
-    x = torch.randn(bs, 3, 224, 224, generator=torch.Generator().manual_seed(1))
-    torch_ref.resnet_forward(arch, sd, x[:2])  # warm-up
-    n_img, t0 = 0, time.perf_counter()
-    while True:
+    x = torch.randn(batch, 3, 224, 224, generator=torch.Generator().manual_seed(1))
+    t0 = time.perf_counter()
+    torch_ref.resnet_forward(arch, sd, x)  # warm-up (one full batch)
+    warm = time.perf_counter() - t0
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
         torch_ref.resnet_forward(arch, sd, x)
-        n_img += bs
-        el = time.perf_counter() - t0
-        if el >= budget_s or n_img >= 4096:
-            break
-    del np
-    return {"value": round(n_img / el, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": "%d images (batches of %d) of the fp32 torch-CPU reference forward on the same "
-                      "fake-quantized %s, %.1f s" % (n_img, bs, arch, el)}
+        ts.append(time.perf_counter() - t0)
+    el = sum(ts)
+    return {"value": round(batch * iters / el, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": "the fp32 torch-CPU reference forward of %s on the same fake-quantized weights, batch %d, "
+                      "1 warm-up (%.2f s) + %d timed iterations (%s s), %d torch threads on %s"
+                      % (arch, batch, warm, iters, "/".join("%.2f" % t for t in ts), threads, _cpu_model())}
+
+
+# the int8-fused roofline of the quantized convs (int8 activations between convs,
+# BN / ReLU / residual fused), per config at the batch it is quoted for, ms
+INT8_FUSED_FLOOR_MS = {"r50_mixed": (256, 0.666), "r18_u8": (256, 0.179), "r34_4bit": (512, 0.742)}
 
 
 def main():
@@ -206,7 +228,7 @@ def main():
     ap.add_argument("--roofline-steps", type=int, default=3, help="eager steps timed per launch for the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--layers", action="store_true", help="print a per-launch roofline table (stderr)")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-iters", type=int, default=2, help="timed CPU-baseline iterations (after 1 warm-up)")
     ap.add_argument("--chunk", type=int, default=None, help="images per pass (Infinity-Cache blocking)")
     ap.add_argument("--streams", type=int, default=None,
                     help="batch slices run concurrently on their own streams (default: engine.STREAMS)")
@@ -378,6 +400,11 @@ def main():
     if args.layers and rank == 0:
         (whole or timer).print_layers(args.roofline_steps)
     attach_traffic(roof, args.config, args.limbs, args.batch, nst if sliced else 1)
+    # how far the north star is: BASELINE.md's int8-fused floor of this config (1-byte activations
+    # between the quantized convs) over the measured step, beside the 3-byte-format frac above
+    fb, fms = INT8_FUSED_FLOOR_MS[args.config]
+    roof["int8_fused_floor_ms"] = round(fms * args.batch / fb, 4)
+    roof["int8_fused_frac"] = round(roof["int8_fused_floor_ms"] / ms_per_step, 4)
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -410,7 +437,7 @@ def main():
             "roofline": roof,
         }
         if not args.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(arch, assign, args.cpu_budget)
+            res["cpu_baseline"] = cpu_baseline(arch, assign, args.batch, args.cpu_iters)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

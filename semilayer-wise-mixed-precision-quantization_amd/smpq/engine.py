@@ -677,7 +677,9 @@ def _capture_locked(model, x_in, cal):
     if pool is None or pool[0] != x_in.device:
         pool = model._smpq_pool = (x_in.device, torch.cuda.graph_pool_handle())
     torch.cuda.synchronize()
-    with torch.cuda.graph(g, pool=pool[1]):
+    # thread_local: only THIS thread's unsafe calls break the capture; other threads' CUDA calls
+    # (a DataLoader's pin-memory thread allocating pinned host memory) stay legal
+    with torch.cuda.graph(g, pool=pool[1], capture_error_mode="thread_local"):
         ctx.overflow = torch.zeros(2, dtype=torch.int32, device=x_in.device)
         ctx.pending_check = lambda: cal[3].check(ctx.overflow[1:])
         y_static = _forward(model, x_in, ctx)
@@ -688,11 +690,29 @@ def _capture_locked(model, x_in, cal):
     return g, ctx, y_static
 
 
-def _graph_forward(model, x, cal):
+def _capture_graph_for(model, x, cal):
+    """Capture the static forward of ``x`` (every cache already warm: an eager forward of the same
+    calibration ran first): on the input's own memory when it has a per-address slot left,
+    otherwise as the fallback graph reading a static copy of the input."""
+    per_ptr = _graphs(model, cal)
+    ak = _addr_key(x)
+    same_shape = sum(1 for k in per_ptr if k != "base" and k[:3] == ak[:3]) if ak is not None else 0
+    if ak is not None and same_shape < GRAPHS_PER_MODEL[0]:
+        per_ptr[ak] = _capture(model, x, cal)
+        return
+    static_x = x.contiguous().clone()
+    g, ctx, y_static = _capture(model, static_x, cal)
+    model._smpq_graph = (_graph_key(model, x, cal), g, static_x, ctx, y_static)
+
+
+def _graph_forward(model, x, cal, capture=True):
     """Static forward through a captured HIP graph; returns (logits, overflow flag tensor). The
     graph reads the input where it lies when its (contiguous) input's address has a graph of its
     own (captured on first sight, up to GRAPHS_PER_MODEL addresses per input shape, dropped with
-    the calibration); otherwise the input is copied into the fallback graph's static buffer."""
+    the calibration); otherwise the input is copied into the fallback graph's static buffer.
+    Without a graph for ``x`` the forward runs eagerly, and the graph is captured right after it
+    (``capture``) or left to the caller (``_capture_graph_for``, once a data-parallel group has
+    agreed that this calibration stays)."""
     key = _graph_key(model, x, cal)
     per_ptr = _graphs(model, cal)
     ak = _addr_key(x)
@@ -703,22 +723,13 @@ def _graph_forward(model, x, cal):
         stats["graph_replays"] += 1
         return y_static.clone(), ctx.overflow
     same_shape = sum(1 for k in per_ptr if k != "base" and k[:3] == ak[:3]) if ak is not None else 0
-    if ak is not None and same_shape < GRAPHS_PER_MODEL[0]:
-        y, ovf = _static_eager(model, x, cal)  # warm every cache outside the capture
-        if any(ovf.tolist()):
-            return y, ovf
-        g, ctx, y_static = _capture(model, x, cal)
-        per_ptr[ak] = (g, ctx, y_static)
-        return y, ovf
     entry = getattr(model, "_smpq_graph", None)
-    if entry is None or entry[0] != key:
-        model._smpq_graph = None
-        y, ovf = _static_eager(model, x, cal)
-        if any(ovf.tolist()):
-            return y, ovf
-        static_x = x.contiguous().clone()
-        g, ctx, y_static = _capture(model, static_x, cal)
-        model._smpq_graph = (key, g, static_x, ctx, y_static)
+    if (ak is not None and same_shape < GRAPHS_PER_MODEL[0]) or entry is None or entry[0] != key:
+        if not (ak is not None and same_shape < GRAPHS_PER_MODEL[0]):
+            model._smpq_graph = None
+        y, ovf = _static_eager(model, x, cal)  # warm every cache outside the capture
+        if capture and not any(ovf.tolist()):
+            _capture_graph_for(model, x, cal)
         return y, ovf
     _, g, static_x, ctx, y_static = entry
     static_x.copy_(x)
@@ -767,13 +778,19 @@ def forward_fused(model, x):
         # the graph replay is enqueued before the host's signature walk.
         y = ovf = None
         need_local = True
+        deferred_capture = False
         if cal is not None and not fresh:
             if USE_GRAPH[0] and _graph_ready(model, x, cal):
                 y, ovf = _graph_forward(model, x, cal)
                 need_local = _signature(model) != cal[1]
             elif cal[1] == _signature(model):
+                # no graph for this input yet: an eager forward only; the capture waits until the
+                # ranks have agreed below that this calibration stays (a capture that
+                # another rank's calibration would discard is not paid for)
                 need_local = False
-                y, ovf = _graph_forward(model, x, cal) if USE_GRAPH[0] else _static_eager(model, x, cal)
+                y, ovf = _graph_forward(model, x, cal, capture=False) if USE_GRAPH[0] else \
+                    _static_eager(model, x, cal)
+                deferred_capture = USE_GRAPH[0] and not _graph_ready(model, x, cal)
         flags = torch.zeros(4, dtype=torch.int32, device=x.device)
         if ovf is not None:
             flags[:2].copy_(ovf)
@@ -783,8 +800,10 @@ def forward_fused(model, x):
             flags[3] = 1
         overflow, stale, need, fresh_any = _dp_max_(flags).tolist()
         if need or fresh_any:
-            return calibrate(model, x, fresh=bool(fresh_any))
+            return calibrate(model, x, stale=bool(stale), fresh=bool(fresh_any))
         if not overflow and not stale:
+            if deferred_capture:
+                _capture_graph_for(model, x, cal)
             return y
         stats["stale_reruns" if stale else "overflow_reruns"] += 1
         return calibrate(model, x, stale=bool(stale))

@@ -24,46 +24,68 @@ from .qconv import find_owner
 # forward (smpq.engine.forward_fused), evaluation or checkpoint save, which raise the
 # ZeroDivisionError there. SMPQ_QUANT_DEFER=0 restores the synchronous check per call.
 DEFER = [os.environ.get("SMPQ_QUANT_DEFER", "1") != "0"]
-_DEV = {}  # device -> {"bits": int8 [17] = 0..16, "status": int32 [1], "scratch": fp32 [1], "pending": n}
+# deferred calls between two checks: each has its own status word, so that check_pending can tell
+# WHICH calls met a constant channel and undo exactly their metadata; a full ring is
+# checked (one host sync per _RING calls)
+_RING = 4096
+_DEV = {}  # device -> {"bits": int8 [17] = 0..16, "status": int32 [_RING], "scratch": fp32 [1], "pending": [...]}
 
 
 def _dev_state(device):
     st = _DEV.get(device)
     if st is None:
         st = _DEV[device] = {"bits": torch.arange(17, dtype=torch.int8, device=device),
-                             "status": torch.zeros(1, dtype=torch.int32, device=device),
-                             "scratch": torch.zeros(1, dtype=torch.float32, device=device), "pending": 0}
+                             "status": torch.zeros(_RING, dtype=torch.int32, device=device),
+                             "scratch": torch.zeros(1, dtype=torch.float32, device=device), "pending": []}
     return st
 
 
 def check_pending(device=None):
     """Raise ZeroDivisionError if a deferred channel_wise_quantizationperchan call (on ``device``,
     or any) met a constant channel (functions.py:40). One host sync, and only while calls are
-    pending; the flag is cleared either way."""
+    pending; the flags are cleared either way. The failing calls changed nothing (the kernel leaves
+    a constant channel's weights and step untouched, as the reference's raise at functions.py:40
+    does), and their bit-width metadata is restored here before raising, so bit_assignment,
+    fully_quantized and checkpoint sidecars never report a channel that was not quantized. Calls
+    made AFTER the failing one (before this check) were applied: the reference would not have
+    reached them — the deferred error surfaces at the next forward, evaluation or save."""
     for dev, st in list(_DEV.items()):
         if (device is not None and dev != device) or not st["pending"]:
             continue
-        n, st["pending"] = st["pending"], 0
-        if int(st["status"].item()):
-            st["status"].zero_()
-            raise ZeroDivisionError("float division by zero (a constant channel in one of the last %d "
-                                    "channel_wise_quantizationperchan calls, functions.py:40)" % n)
+        pend, st["pending"] = st["pending"], []
+        flags = st["status"][:len(pend)].tolist()
+        if not any(flags):
+            continue
+        st["status"].zero_()
+        bad = 0
+        # newest first: a channel quantized twice in the pending window gets its oldest bit back
+        for (owner, ch, prev), f in reversed(list(zip(pend, flags))):
+            if f:
+                bad += 1
+                if owner is not None:
+                    owner.record_quant_inplace(ch, prev)
+        raise ZeroDivisionError("float division by zero (a constant channel in %d of the last %d "
+                                "channel_wise_quantizationperchan calls, functions.py:40)" % (bad, len(pend)))
 
 
 def _quantize_row_deferred(tensor, bit, i):
     """One channel of a contiguous fp32 device weight, no host sync (see DEFER)."""
     row = tensor[i]
     st = _dev_state(tensor.device)
+    if len(st["pending"]) >= _RING:
+        check_pending(tensor.device)
     owner = find_owner(tensor)
     if owner is not None and owner.qstep.device != tensor.device:
         owner = None
     step = owner.qstep[i:i + 1] if owner is not None else st["scratch"]
+    k = len(st["pending"])
     lib = _lib.load()
     with torch.cuda.device(tensor.device):
         _lib.check(lib.smpq_quantize_channels_ex(_lib.ptr(row), 1, row.numel(), st["bits"].data_ptr() + int(bit),
-                                                 _lib.ptr(step), _lib.ptr(st["status"]), ops._qsem(None, True),
-                                                 _lib.stream_ptr()), "smpq_quantize_channels_ex")
-    st["pending"] += 1
+                                                 _lib.ptr(step), st["status"].data_ptr() + 4 * k,
+                                                 ops._qsem(None, True), _lib.stream_ptr()),
+                   "smpq_quantize_channels_ex")
+    st["pending"].append((owner, int(i), int(owner._bits_host[i]) if owner is not None else 0))
     if owner is not None:
         owner.record_quant_inplace(int(i), int(bit))  # qstep[i] was written by the kernel
     return tensor

@@ -148,11 +148,20 @@ def test_deferred_channel_quantizer(gpu):
     with torch.no_grad():
         conv2.weight.data[7] = 0.25
     before = conv2.weight.detach().clone()
+    # channel 3 quantized before and after (applied), channel 7 constant (its metadata restored)
+    functions.channel_wise_quantizationperchan(conv2.weight.data, 6, 3)
+    functions.channel_wise_quantizationperchan(conv2.weight.data, 4, 5)
+    meta = (conv2.qbits.clone(), conv2.qstep.clone(), conv2._bits_host.copy())
     functions.channel_wise_quantizationperchan(conv2.weight.data, 8, 7)
+    functions.channel_wise_quantizationperchan(conv2.weight.data, 4, 3)
     with pytest.raises(ZeroDivisionError):
         with torch.no_grad():
             net(x)
     assert torch.equal(conv2.weight.detach()[7], before[7])
+    # the failed channel is not reported as quantized; the later call stays applied
+    assert conv2.qbits[7].item() == meta[0][7].item() == 0 and conv2._bits_host[7] == 0
+    assert torch.equal(conv2.qstep[7], meta[1][7]) and not conv2.fully_quantized()
+    assert conv2.qbits[3].item() == 4 and conv2.qbits[5].item() == 4
     quant.check_pending()  # cleared by the raise
     # the synchronous path (DEFER off) raises in the call, as the reference does
     quant.DEFER[0] = False

@@ -162,3 +162,28 @@ def test_host_batches_staged_during_graph_capture(gpu):
     ref = functions.evaluate_acc_loss_softmax(net, gpu, on_dev)
     for r in runs:
         assert r[0] == ref[0] and r[1] == ref[1] and all(torch.equal(a, b) for a, b in zip(r[2], ref[2]))
+
+
+def test_pinned_dataloader_batches_during_graph_capture(gpu):
+    """the reference's loader (imagenet.py:36-40: num_workers=16, pin_memory=True) pins
+    each batch on torch's pin-memory THREAD, which allocates pinned host memory while the main
+    thread may be capturing a HIP graph. engine._capture uses capture_error_mode='thread_local',
+    so those calls stay legal; the results equal the device-resident loader's bit for bit and
+    graphs were captured meanwhile."""
+    import functions
+    from smpq import stats
+    from test_gpu import build_model
+    net = build_model(gpu, "resnet18", "r18_u8")
+    g = torch.Generator().manual_seed(17)
+    xs = torch.randn(36, 3, 224, 224, generator=g)
+    ys = torch.randint(0, 1000, (36,), generator=g)
+    ds = torch.utils.data.TensorDataset(xs, ys)
+    loader = torch.utils.data.DataLoader(ds, batch_size=6, shuffle=False, num_workers=2, pin_memory=True,
+                                         multiprocessing_context="fork")
+    on_dev = [(xs[i:i + 6].to(gpu), ys[i:i + 6].to(gpu)) for i in range(0, 36, 6)]
+    c0 = stats["graph_captures"]
+    runs = [functions.evaluate_acc_loss_softmax(net, gpu, loader) for _ in range(2)]
+    assert stats["graph_captures"] > c0
+    ref = functions.evaluate_acc_loss_softmax(net, gpu, on_dev)
+    for r in runs:
+        assert r[0] == ref[0] and r[1] == ref[1] and all(torch.equal(a, b) for a, b in zip(r[2], ref[2]))
