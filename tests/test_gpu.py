@@ -1279,3 +1279,55 @@ def test_bench_workload_parity_full_size(gpu, case, arch, assign, batch):
     assert err <= 2e-4, err
     assert per_img <= PER_IMAGE_RTOL, per_img
     assert torch.equal(y.argmax(1), ref.argmax(1)), agree
+
+
+@pytest.mark.parametrize("arch,assign", [("resnet50", "r50_mixed"), ("resnet18", "r18_u8")])
+def test_check_stream_fork_capture_replay(gpu, arch, assign):
+    """Verdict r5 item 2: the capture topology of commit a082ca2 — the weights' content check on a
+    stream forked from the capture stream only for it, beside the downsample side-stream forks
+    (STREAMS 1) or the batch-slice forks (STREAMS 2, 3), joined before EndCapture — which crashed
+    one CUDAGraph.replay() in round 5's GPU suite. Every fork is one level deep (the topology ROCm
+    7.2 captures: tools/repro_graph_fork.py); captured and replayed here in the test's call order,
+    bitwise equal to the serial eager forward."""
+    from smpq import engine
+    net = build_model(gpu, arch, assign)
+    x = torch.randn(7, 3, 224, 224, generator=torch.Generator().manual_seed(23)).to(gpu)
+    x2 = torch.randn(7, 3, 224, 224, generator=torch.Generator().manual_seed(24)).to(gpu)
+    shipped = engine._capture_locked
+
+    def capture_with_check_stream(model, x_in, cal):
+        g = torch.cuda.CUDAGraph()
+        ctx = engine.Ctx(x_in.shape[0], x_in.device, ranges=cal[0], cache=cal[2])
+        pool = getattr(model, "_smpq_pool", None)
+        if pool is None or pool[0] != x_in.device:
+            pool = model._smpq_pool = (x_in.device, torch.cuda.graph_pool_handle())
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, pool=pool[1], capture_error_mode="thread_local"):
+            ctx.overflow = torch.zeros(2, dtype=torch.int32, device=x_in.device)
+            main = torch.cuda.current_stream()
+            chk = engine._stream((x_in.device, "check"))
+            chk.wait_stream(main)
+            with torch.cuda.stream(chk):
+                cal[3].check(ctx.overflow[1:])
+            y_static = engine._forward(model, x_in, ctx)
+            main.wait_stream(chk)
+        engine.stats["graph_captures"] += 1
+        return g, ctx, y_static
+
+    old = engine.CONCURRENT_DS[0], engine.USE_GRAPH[0], engine.STREAMS[0]
+    got = []
+    try:
+        engine._capture_locked = capture_with_check_stream
+        with torch.no_grad():
+            engine.CONCURRENT_DS[0], engine.USE_GRAPH[0], engine.STREAMS[0] = False, False, 1
+            net(x)  # calibrate
+            a, a2 = net(x), net(x2)
+            for streams in (1, 2, 3):
+                engine.STREAMS[0], engine.CONCURRENT_DS[0], engine.USE_GRAPH[0] = streams, True, True
+                got += [(net(x), a), (net(x2), a2), (net(x), a), (net(x2), a2)]  # 2 captures, 2 replays
+    finally:
+        engine._capture_locked = shipped
+        engine.CONCURRENT_DS[0], engine.USE_GRAPH[0], engine.STREAMS[0] = old
+    torch.cuda.synchronize()
+    for i, (g, want) in enumerate(got):
+        assert torch.equal(g, want), i
