@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SMPQ_ABI_VERSION 5
+#define SMPQ_ABI_VERSION 6
 
 /* status codes */
 #define SMPQ_OK 0

@@ -364,299 +364,9 @@ int launch_halo_l(int cfg, const ConvArgs& a, hipStream_t s) {
 
 }  // namespace
 
-// ---- virtual-row tiles (round 5): one MFMA pixel fragment = one 16-lane virtual row -----------
-// The halo tiles above take fragments of 16 consecutive tile pixels in row-major order, which for
-// tile widths that are not a multiple of 4 (7 x 14 at 14^2) spread a fragment over three patch
-// rows and give 2-way LDS bank conflicts on most B-fragment reads (tools/halo_conflicts.py); the
-// 7^2 images fit them only with a quarter of every fragment empty. Here a tile is TH rows of a
-// 16-lane virtual row holding 16 / SW images side by side, each in a slot of SW lanes (SW = 16:
-// one image up to 16 wide, the 14^2 convs; SW = 8: two images up to 7 wide, the 7^2 convs):
-// lane v of fragment (row) f is output pixel (row oh0 + f, column v % SW) of image img0 + v / SW.
-// The patch is [L][TH + 2][18][64]: patch column j holds image column j - 1 - SW * s of slot
-// s = (j - 1) / SW (zero outside the image; with two slots the column between them is the right
-// pad of the first and the left pad of the second image), so tap (kr, kc) of lane v is patch
-// pixel (f + kr, v + kc) in every slot. A patch pixel's 16-B chunk c is stored at
-// c ^ 2 * ((j >> 2) & 1): every tap's ds_read_b128 is bank-conflict-free (checked exhaustively,
-// tools/halo_conflicts.py --vrow). The rest is the kernel above: per 64-channel input chunk the
-// patch of every limb and the nine taps' weights are staged once, nine taps run out of LDS, and
-// the lean static-range epilogue is the implicit-GEMM kernel's, bitwise.
-struct HaloVCfg {
-  int th, sw, nst;  // rows per tile, slot width (16: one image, 8: two images), LDS stages
-};
-constexpr HaloVCfg kHaloV[] = {
-    {7, 16, 1},  // 14^2: half an image (7 x 14 of 7 x 16 lanes)
-    {7, 8, 1},   // 7^2: two images (2 x 7 x 7 of 7 x 16 lanes)
-    {7, 16, 2},  // as 0, chunk k + 1 prefetched
-    {7, 8, 2},   // as 1, prefetched
-};
-constexpr int kNumHaloV = sizeof(kHaloV) / sizeof(kHaloV[0]);
-
-namespace {
-
-constexpr int kVPW = 18;  // patch columns: 16 lanes + the taps' two extra columns
-
-__device__ __forceinline__ int vswz(int j) { return 2 * ((j >> 2) & 1); }
-
-template <int L, int TH, int SW, int NST, bool OFF>
-__global__ __launch_bounds__(64 * TH) void qconv_halo_vrow_kernel(ConvArgs a, int nct, int nrt) {
-  constexpr int NWV = TH;  // one fragment (virtual row) per wave
-  constexpr int IPT = 16 / SW;
-  constexpr int PH = TH + 2;
-  constexpr int PLIMB = PH * kVPW * 64;
-  constexpr int PB = (L * PLIMB + 1023) / 1024 * 1024;
-  constexpr int STAGE = kHaloWB + PB;
-  constexpr int PPIECE = PB / 1024;
-  constexpr int WSL = (36 + NWV - 1) / NWV, PSL = (PPIECE + NWV - 1) / NWV;
-  extern __shared__ __attribute__((aligned(1024))) int8_t lds[];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  __builtin_assume(wave >= 0 && wave < NWV);
-  const int frow = lane & 15, grp = lane >> 4;
-
-  // ---- tile (XCD-aware order, as above): channel tile, then row tile, then image group --------
-  const int total = gridDim.x, bid = blockIdx.x;
-  const int full = total & ~7;
-  int t = bid;
-  if (t < full) t = (t & 7) * (full >> 3) + (t >> 3);
-  const int ct = t % nct, s = t / nct;
-  const int ig = s / nrt, rt = s - ig * nrt;
-  const int img0 = ig * IPT, oh0 = rt * TH;
-  const int nch = a.cin / 64;
-
-  const v4i wrs = make_rsrc(a.codes, a.wplane);
-  const v4i xrs = make_rsrc(a.xq, (long long)L * a.plane);
-
-  unsigned wsrc[WSL], psrc[PSL];
-  {
-    const int row = lane >> 2;
-    const int lc = (lane & 3) ^ swz<64>(row);
-    const unsigned rowoff = a.w_kmajor ? (unsigned)((ct * 64 + row) * 64 + 16 * lc)
-                                       : (unsigned)((ct * 64 + row) * a.K + 16 * lc);
-    const unsigned tapstride = a.w_kmajor ? (unsigned)(nch * a.cout * 64) : (unsigned)a.cin;
-    const unsigned blkstride = a.w_kmajor ? 16u * 64u : 16u * (unsigned)a.K;
-#pragma unroll
-    for (int k = 0; k < WSL; ++k) {
-      const int p = wave + NWV * k;
-      wsrc[k] = p < 36 ? rowoff + (unsigned)(p >> 2) * tapstride + (unsigned)(p & 3) * blkstride : kOOB;
-    }
-  }
-  {
-    // patch piece q = LDS bytes [1024 q, +1024) of the [L][PH][18][64] image: pixels 16 q .. 16 q + 15,
-    // 4 lanes per pixel; the divisions are by compile-time constants
-    const unsigned plane = (unsigned)a.plane;
-#pragma unroll
-    for (int k = 0; k < PSL; ++k) {
-      const int q = wave + NWV * k;
-      const int P = 16 * q + (lane >> 2);
-      const int l = P / (PH * kVPW), rem = P - l * (PH * kVPW);
-      const int pr = rem / kVPW, j = rem - pr * kVPW;
-      const int sl = (j - 1) / SW, x = j - 1 - sl * SW;  // j >= 1 checked below
-      const int img = img0 + sl, ih = oh0 - 1 + pr;
-      const bool ok = q < PPIECE && l < L && j >= 1 && sl < IPT && x < a.w && img < a.n && ih >= 0 && ih < a.h;
-      const int c16 = 16 * ((lane & 3) ^ vswz(j));
-      psrc[k] = ok ? (unsigned)l * plane + (unsigned)(((img * a.h + ih) * a.w + x) * a.cin + c16) : kOOB;
-    }
-  }
-  const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
-  const unsigned wchunk = __builtin_amdgcn_readfirstlane(a.w_kmajor ? (unsigned)(a.cout * 64) : 64u);
-  auto issue = [&](int cc, int stage) {
-    const unsigned sb = lds0 + stage * STAGE;
-#pragma unroll
-    for (int k = 0; k < WSL; ++k)
-      if (wave + NWV * k < 36)
-        dma16(sb + (wave + NWV * k) * 1024, wrs, wsrc[k], __builtin_amdgcn_readfirstlane((unsigned)cc * wchunk));
-#pragma unroll
-    for (int k = 0; k < PSL; ++k)
-      if (wave + NWV * k < PPIECE)
-        dma16(sb + kHaloWB + (wave + NWV * k) * 1024, xrs, psrc[k], __builtin_amdgcn_readfirstlane((unsigned)cc * 64u));
-  };
-
-  // ---- per-lane fragment bases: A + tap * 4096 + i * 1024; B + l * PLIMB + kr * 18 * 64 --------
-  const int wrd = frow * 64 + 16 * (grp ^ swz<64>(frow));
-  int bkc[3];
-#pragma unroll
-  for (int kc = 0; kc < 3; ++kc) bkc[kc] = kHaloWB + (wave * kVPW + frow + kc) * 64 + 16 * (grp ^ vswz(frow + kc));
-
-  v4i acc[L][4];
-  constexpr bool do_off = OFF;
-  int rs[L];
-#pragma unroll
-  for (int l = 0; l < L; ++l) rs[l] = 0;
-
-  auto compute = [&](const int8_t* sb, auto first) {
-#pragma unroll
-    for (int kr = 0; kr < 3; ++kr)
-#pragma unroll
-      for (int kc = 0; kc < 3; ++kc) {
-        const int tap = kr * 3 + kc;
-        v4i fa[4], fb[L];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const v4i*>(sb + wrd + tap * 4096 + i * 1024);
-#pragma unroll
-        for (int l = 0; l < L; ++l) fb[l] = *reinterpret_cast<const v4i*>(sb + bkc[kc] + l * PLIMB + kr * kVPW * 64);
-        if constexpr (do_off) {
-#pragma unroll
-          for (int l = 0; l < L; ++l) {
-            int sacc = rs[l];
-            sacc = __builtin_amdgcn_sdot4(fb[l].x, 0x01010101, sacc, false);
-            sacc = __builtin_amdgcn_sdot4(fb[l].y, 0x01010101, sacc, false);
-            sacc = __builtin_amdgcn_sdot4(fb[l].z, 0x01010101, sacc, false);
-            sacc = __builtin_amdgcn_sdot4(fb[l].w, 0x01010101, sacc, false);
-            rs[l] = sacc;
-          }
-        }
-#pragma unroll
-        for (int l = 0; l < L; ++l)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[l][i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
-                fa[i], fb[l], (decltype(first)::value && tap == 0) ? v4i{0, 0, 0, 0} : acc[l][i], 0, 0, 0);
-      }
-  };
-
-  using First = std::integral_constant<bool, true>;
-  using Later = std::integral_constant<bool, false>;
-  if constexpr (NST == 1) {
-    issue(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    compute(lds, First{});
-    for (int cc = 1; cc < nch; ++cc) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      issue(cc, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      compute(lds, Later{});
-    }
-  } else {
-    issue(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (nch > 1) issue(1, 1);
-    compute(lds, First{});
-    for (int cc = 1; cc < nch; ++cc) {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (cc + 1 < nch) issue(cc + 1, (cc + 1) & 1);
-      compute(lds + (cc & 1) * STAGE, Later{});
-    }
-  }
-
-  // ---- epilogue: the lean static-range epilogue (as the kernel above, one fragment per wave) ---
-  if constexpr (do_off) {
-#pragma unroll
-    for (int l = 0; l < L; ++l) {
-      int sacc = rs[l];
-      sacc += __shfl_xor(sacc, 16, kWave);
-      sacc += __shfl_xor(sacc, 32, kWave);
-      rs[l] = sacc;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int4 coff = *reinterpret_cast<const int4*>(a.w_off + ct * 64 + 16 * i + 4 * grp);
-      const int cor[4] = {coff.x, coff.y, coff.z, coff.w};
-#pragma unroll
-      for (int l = 0; l < L; ++l)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[l][i][r] += __mul24(cor[r], rs[l]);
-    }
-  }
-  const long long oplane = (long long)a.M * a.cout;
-  const int sl = frow / SW, ow = frow - sl * SW;
-  const int img = img0 + sl, oh = oh0 + wave;
-  const bool ok = sl < IPT && img < a.n && ow < a.wo && oh < a.ho;
-  const unsigned qoff = ok ? (unsigned)(((long long)(img * a.ho + oh) * a.wo + ow) * a.cout + ct * 64 + 16 * grp) : kOOB;
-  constexpr float qmax = act_qmax<L>();
-  const float rscale = ok ? a.x_absmax[img] * a.inv_qmax : 0.f;
-  const float inv = a.yq_inv;
-  constexpr float lo = 0.f;
-  constexpr bool relu = true;
-  unsigned wq[4][L];
-  float vmax = 0.f;
-  const int rq_dummy[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = ct * 64 + 16 * i + 4 * grp;
-    const float4 cs = *reinterpret_cast<const float4*>(a.col_scale + c);
-    const float4 csh = *reinterpret_cast<const float4*>(a.col_shift + c);
-    const float csq[4] = {cs.x * inv, cs.y * inv, cs.z * inv, cs.w * inv};
-    const float shq[4] = {csh.x * inv, csh.y * inv, csh.z * inv, csh.w * inv};
-    v4i accq[L];
-#pragma unroll
-    for (int l = 0; l < L; ++l) accq[l] = acc[l][i];
-    const float m = lean_quad<L, L, 0>(accq, rscale, csq, shq, false, rq_dummy, 0.f, relu, lo, wq[i]);
-    vmax = ok ? fmaxf(vmax, m) : vmax;
-  }
-  const v4i qrs4 = make_rsrc(a.yq, (long long)L * oplane);
-  const bool nt = __builtin_amdgcn_readfirstlane(a.nt_store) != 0;
-#pragma unroll
-  for (int l = 0; l < L; ++l) {
-    unsigned w0 = wq[0][l], w1 = wq[1][l], w2 = wq[2][l], w3 = wq[3][l];
-    transpose4(w0, w1, w2, w3);
-    store_limbs16(v4u{w0, w1, w2, w3}, qrs4, qoff, __builtin_amdgcn_readfirstlane((unsigned)((long long)l * oplane)), nt);
-  }
-  if (__any(vmax > qmax) && lane == 0) atomicMax(a.overflow, 1);
-}
-
-template <int L, int TH, int SW, int NST>
-int launch_halo_vrow_one(const ConvArgs& a, hipStream_t stream) {
-  constexpr int IPT = 16 / SW;
-  if ((IPT > 1 && a.w > SW - 1) || (IPT == 1 && a.w > 16))
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: image too wide for this virtual-row halo tile");
-  const int nrt = (a.ho + TH - 1) / TH, nig = (a.n + IPT - 1) / IPT, nct = a.cout / 64;
-  const long long blocks = (long long)nig * nrt * nct;
-  if (blocks > 0x7fffffffLL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
-  constexpr int stage = kHaloWB + (L * (TH + 2) * kVPW * 64 + 1023) / 1024 * 1024;
-  const int nch = a.cin / 64;
-  const int lds_bytes = (nch < NST ? nch : NST) * stage;
-  constexpr int kMax = NST * stage;
-  static_assert(kMax <= 160 * 1024, "LDS per CU");
-  auto k0 = qconv_halo_vrow_kernel<L, TH, SW, NST, false>;
-  auto k1 = qconv_halo_vrow_kernel<L, TH, SW, NST, true>;
-  auto set_lds = [](const void* k) {
-    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kMax);
-    if (e != hipSuccess) (void)hipGetLastError();
-    return e;
-  };
-  static const hipError_t attr0 = set_lds(reinterpret_cast<const void*>(k0));
-  static const hipError_t attr1 = set_lds(reinterpret_cast<const void*>(k1));
-  const bool off = a.has_offset != 0;
-  if ((off ? attr1 : attr0) != hipSuccess) return check_hip(off ? attr1 : attr0, "qconv_halo_vrow_kernel LDS attribute");
-  auto k = off ? k1 : k0;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * TH), lds_bytes, stream, a, nct, nrt);
-  return check_hip(hipGetLastError(), "qconv_halo_vrow_kernel launch");
-}
-
-template <int L>
-int launch_halo_vrow_l(int cfg, const ConvArgs& a, hipStream_t s) {
-  switch (cfg) {
-    case 0: return launch_halo_vrow_one<L, 7, 16, 1>(a, s);
-    case 1: return launch_halo_vrow_one<L, 7, 8, 1>(a, s);
-    case 2: return launch_halo_vrow_one<L, 7, 16, 2>(a, s);
-    case 3: return launch_halo_vrow_one<L, 7, 8, 2>(a, s);
-    default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad halo tile config");
-  }
-}
-
-}  // namespace
-
-int halo_num_cfgs() { return kNumHalo + kNumHaloV; }
+int halo_num_cfgs() { return kNumHalo; }
 
 void halo_cfg_info(int cfg, int* bm, int* bn, int* threads) {
-  if (cfg >= kNumHalo) {  // virtual-row tiles: TH rows of 16 lanes
-    const HaloVCfg& v = kHaloV[cfg - kNumHalo];
-    *bm = v.th * 16;
-    *bn = 64;
-    *threads = 64 * v.th;
-    return;
-  }
   const HaloCfg& c = kHalo[cfg];
   *bm = c.th * c.tw;  // pixels
   *bn = 64;           // channels
@@ -671,19 +381,12 @@ bool halo_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int w
 }
 
 int launch_halo(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s) {
-  if (cfg < 0 || cfg >= kNumHalo + kNumHaloV) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad halo tile config");
+  if (cfg < 0 || cfg >= kNumHalo) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: bad halo tile config");
   if (!halo_supported(cfg, a.cin, a.cout, a.kh, a.kw, limbs, wlimbs) || a.stride != 1 || a.pad != 1 || a.s2d)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: halo tiles take 3x3 / stride 1 / pad 1 convs with cin % 64 == 0, "
                                 "cout % 64 == 0 and one weight limb");
   if (!a.yq || a.y || a.residual || a.res_q || a.y_absmax || !a.relu)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: halo tiles run the static-range limb-plane epilogue with ReLU only");
-  if (cfg >= kNumHalo) {
-    switch (limbs) {
-      case 2: return launch_halo_vrow_l<2>(cfg - kNumHalo, a, s);
-      case 3: return launch_halo_vrow_l<3>(cfg - kNumHalo, a, s);
-      default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: halo tiles need 2 or 3 activation limbs");
-    }
-  }
   switch (limbs) {
     case 2: return launch_halo_l<2>(cfg, a, s);
     case 3: return launch_halo_l<3>(cfg, a, s);

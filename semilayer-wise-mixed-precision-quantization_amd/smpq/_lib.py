@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must be imported before the library; see module doc
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsmpq.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lib = None
 _lock = threading.Lock()

@@ -10,12 +10,6 @@ from test_gpu import make_layer
 pytestmark = pytest.mark.gpu
 
 
-def _vrow_cfgs(ops):
-    """The virtual-row halo configs: the last four halo tile configs (conv_halo.hip kHaloV follows
-    kHalo): one image up to 16 wide, two images up to 7 wide, and both with a prefetched chunk."""
-    return sorted(c for c in ops.tile_configs() if ops.tile_kind(c) == ops.TILE_HALO3X3)[-4:]
-
-
 def _halo_cfgs(ops, limbs, cin, cout):
     return [c for c in ops.tile_configs()
             if ops.tile_kind(c) == ops.TILE_HALO3X3 and ops._tile_fits(c, limbs, 1, cout, cin, 3)]
@@ -25,9 +19,8 @@ def _halo_cfgs(ops, limbs, cin, cout):
 @pytest.mark.parametrize("limbs", [2, 3])
 @pytest.mark.parametrize("shape", [(64, 64, 56, 56, 2), (128, 128, 28, 28, 3), (256, 256, 14, 14, 2),
                                    (64, 128, 13, 17, 2), (192, 64, 9, 30, 1),
-                                   # the virtual-row tiles' geometries: two 7 x 7 images per tile
-                                   # (an odd image count leaves half a tile empty), one image of
-                                   # width 16 / narrower than 7 / a partial row tile
+                                   # narrow images: 7 x 7 (an odd image count), width 16, narrower
+                                   # than 7, a partial row tile
                                    (512, 512, 7, 7, 3), (64, 128, 9, 16, 2), (128, 64, 5, 6, 3)],
                          ids=lambda s: "c%d_o%d_%dx%d_n%d" % s)
 def test_halo_equals_implicit_gemm(gpu, shape, limbs, relu):
@@ -56,12 +49,8 @@ def test_halo_equals_implicit_gemm(gpu, shape, limbs, relu):
                         ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=relu, tile_cfg=c,
                                      emit_range=rng, overflow=ovf, want_f32=False, weight_layout=layout)
                     continue
-                try:
-                    _, yq = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=relu, tile_cfg=c,
-                                         emit_range=rng, overflow=ovf, want_f32=False, weight_layout=layout)
-                except _lib.SmpqError as e:  # a virtual-row tile refuses images wider than its slots
-                    assert "too wide" in str(e) and c in _vrow_cfgs(ops) and w > 7, (c, e)
-                    continue
+                _, yq = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=relu, tile_cfg=c,
+                                     emit_range=rng, overflow=ovf, want_f32=False, weight_layout=layout)
                 assert torch.equal(yq, yq0), (c, frac, layout)
                 assert torch.equal(ovf, ovf0), (c, frac, layout)
 
@@ -82,41 +71,9 @@ def test_halo_without_offsets_and_repeatable(gpu):
     _, yq0 = ops.conv2d_q(xq, am, codes, None, 3, 3, 1, 1, step, shift, relu=True, emit_range=rng, overflow=ovf,
                           want_f32=False)
     for c in _halo_cfgs(ops, 3, cin, cout):
-        try:
-            ops.conv2d_q(xq, am, codes, None, 3, 3, 1, 1, step, shift, relu=True, tile_cfg=c, emit_range=rng,
-                         overflow=ovf, want_f32=False)
-        except _lib.SmpqError as e:  # virtual-row tiles take images up to 16 (7) wide only
-            assert "too wide" in str(e), (c, e)
-            continue
         outs = [ops.conv2d_q(xq, am, codes, None, 3, 3, 1, 1, step, shift, relu=True, tile_cfg=c, emit_range=rng,
                              overflow=ovf, want_f32=False)[1] for _ in range(20)]
         for yq in outs:
-            assert torch.equal(yq, yq0), c
-    assert int(ovf.item()) == 0
-
-
-@pytest.mark.parametrize("h", [14, 7])
-def test_vrow_halo_repeatable(gpu, h):
-    """The virtual-row tiles at 14^2 (one image per tile) and 7^2 (two images per tile, an odd
-    image count): 20 back-to-back launches give the implicit-GEMM kernel's bits every time."""
-    from smpq import ops
-    cin, cout, n = 256, 128, 5
-    wd, step, codes, offset = make_layer(gpu, cin, cout, 3, seed=h)
-    x = torch.relu(torch.randn(n, h, h, cin, generator=torch.Generator().manual_seed(h))).to(gpu)
-    am = ops.act_absmax(x)
-    xq = ops.act_quantize(x, am, 3)
-    shift = torch.linspace(-0.5, 0.5, cout, device=gpu)
-    ref = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=True)
-    rng = float(ref.abs().max()) * 2
-    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
-    _, yq0 = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=True, emit_range=rng, overflow=ovf,
-                          want_f32=False)
-    vrow = _vrow_cfgs(ops)
-    assert len(vrow) == 4
-    for c in (vrow if h <= 7 else vrow[0::2]):  # the two-image tiles take images up to 7 wide
-        for _ in range(20):
-            _, yq = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=True, tile_cfg=c,
-                                 emit_range=rng, overflow=ovf, want_f32=False)
             assert torch.equal(yq, yq0), c
     assert int(ovf.item()) == 0
 
@@ -149,7 +106,6 @@ def test_model_forward_halo_tiles_bitwise(gpu, arch, assign):
     from test_gpu import build_model
     net = build_model(gpu, arch, assign, None)
     x = torch.randn(5, 3, 224, 224, generator=torch.Generator().manual_seed(7)).to(gpu)
-    vrow = _vrow_cfgs(ops)
     orig = ops._choose_tile
     picked = []
 
@@ -161,9 +117,7 @@ def test_model_forward_halo_tiles_bitwise(gpu, arch, assign):
             # stride|pad|limbs|wlimbs|res_f32|emit_q|want_f32|res_q
             lean = key[5] == 3 and key[7] == 1 and key[12] and not key[13] and not key[14] and not key[11]
             if kind == "halo" and halo and lean:
-                # the virtual-row tiles where the images fit them (conv_halo.hip kHaloV order: one
-                # image up to 16 wide, then two images up to 7 wide)
-                c = vrow[1] if key[2] <= 7 else vrow[0] if key[2] <= 16 else halo[0]
+                c = halo[0]
                 picked.append(c)
                 return c
             return gemm[0] if gemm else None
@@ -184,5 +138,4 @@ def test_model_forward_halo_tiles_bitwise(gpu, arch, assign):
         ops._TUNED.clear()
         engine.USE_GRAPH[0] = True
     assert picked, "no conv ran on a halo tile"
-    assert any(c in vrow for c in picked), "no conv ran on a virtual-row halo tile"
     assert torch.equal(outs["halo"], outs["gemm"])
