@@ -219,8 +219,10 @@ INT8_FUSED_FLOOR_MS = {"r50_mixed": (256, 0.666), "r18_u8": (256, 0.179), "r34_4
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # defaults: 100 timed steps after 20 warm-up steps (~1 s of GPU time): a steady-state rate
+    # (20 / 5 read 1-2 % lower on the same box, profiles/r06_bench_length.txt)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
     ap.add_argument("--config", default="r50_mixed", choices=sorted(CONFIGS))
     ap.add_argument("--limbs", type=int, default=3,

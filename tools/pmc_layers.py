@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Join tools/pmc_layers.sh's two PMC passes to bench.py's layer table: per quantized-conv launch of
-the eager roofline region (the last 53 x 3 dispatches), the instruction mix per wave (VALU, SALU,
+the eager roofline region (the last N x 3 dispatches, N = the launches of a step: 53 for R50), the instruction mix per wave (VALU, SALU,
 LDS, VMEM) against its MFMA cycles, and the wave states. Diagnostics only.
 
 usage: python tools/pmc_layers.py <outdir>"""
@@ -26,14 +26,16 @@ def load(d):
     return [rows[k] for k in sorted(rows)][-N * R:]
 
 
-p1, p2 = load(os.path.join(O, "p1")), load(os.path.join(O, "p2"))
 layers = []
 log = open(os.path.join(O, "p1.log")).read().splitlines()
 try:
     i = next(j for j, l in enumerate(log) if l.startswith("launch"))
+    # the layer table's rows (one per launch of a step) end at its "total" line: N of any config
+    N = next(j for j, l in enumerate(log[i + 1:]) if l.startswith("total"))
     layers = [l[:33] + l[33:43] for l in log[i + 1:i + 1 + N]]
 except StopIteration:
     layers = [""] * N
+p1, p2 = load(os.path.join(O, "p1")), load(os.path.join(O, "p2"))
 groups = {}
 print("%-43s %5s %7s %6s %6s %6s %6s %5s %5s %5s %5s %6s" % (
     "launch (t_us)", "vgpr", "waves", "VALU/w", "SALU/w", "LDS/w", "MFMAc/w", "V/MF", "wait", "istl", "actv", "mfma%"))
