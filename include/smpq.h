@@ -276,10 +276,18 @@ int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads);
  *                              return SMPQ_E_INVALID.
  *                              Its configurations follow the LDS-DMA ones; BM = the tile's pixels
  *                              (TH x TW of one image), BN = 64.
+ *   SMPQ_TILE_RESIDENT1X1      (ABI 6) weight-stationary 1x1 tiles: 1x1 / pad 0 convs with cin 64,
+ *                              cout 256, 3 activation limbs, 1 or 3 weight limbs, no weight offsets,
+ *                              static-range limb-plane output without a residual (yq set; y,
+ *                              y_absmax, residual, residual_q NULL; relu either) — other calls return
+ *                              SMPQ_E_INVALID. A persistent workgroup keeps every weight limb in
+ *                              registers and walks pixel tiles; BM = pixels per tile, BN = 256.
+ *                              Its configurations follow the halo ones.
  * (negative: error code). Values 0 and 1 were the register-staged family (ABI <= 3, removed). */
 #define SMPQ_TILE_LDS_DMA 2
 #define SMPQ_TILE_LDS_DMA_K128 3
 #define SMPQ_TILE_HALO3X3 4
+#define SMPQ_TILE_RESIDENT1X1 5
 int smpq_conv2d_tile_kind(int cfg);
 
 /* 1 if tile configuration cfg can run a conv of this shape and these limb counts (the rules the

@@ -469,6 +469,7 @@ extern "C" int smpq_conv2d_tile_supported(int cfg, int cin, int cout, int kh, in
 extern "C" int smpq_conv2d_tile_kind(int cfg) {
   if (cfg < 0 || cfg >= glds_num_cfgs()) return fail(SMPQ_E_INVALID, "smpq_conv2d_tile_kind: bad config");
   if (glds_is_halo(cfg)) return SMPQ_TILE_HALO3X3;
+  if (glds_is_resident(cfg)) return SMPQ_TILE_RESIDENT1X1;
   return glds_cfg_bk(cfg) == 128 ? SMPQ_TILE_LDS_DMA_K128 : SMPQ_TILE_LDS_DMA;
 }
 

@@ -94,6 +94,13 @@ void halo_cfg_info(int cfg, int* bm, int* bn, int* threads);
 bool halo_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs);
 int launch_halo(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s);
 
+// weight-stationary 1x1 tiles (conv_resident.hip); their configs follow the halo ones
+int resident_num_cfgs();
+void resident_cfg_info(int cfg, int* bm, int* bn, int* threads);
+bool resident_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs);
+int launch_resident(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s);
+bool glds_is_resident(int cfg);
+
 // The 4 codes (channels 0..3) held by one dword per limb plane, w[l] = the 4 balanced digits of
 // limb l: q = sum_l d_l 256^l. With u_l = d_l + 128 (byte ^ 0x80) for the low limbs,
 // q = sext24(u0 | u1 << 8 | d2 << 16) - 0x8080 (L = 3), sext16(u0 | d1 << 8) - 0x80 (L = 2).

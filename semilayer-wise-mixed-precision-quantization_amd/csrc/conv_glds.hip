@@ -17,14 +17,20 @@ SMPQ_GLDS_FAMILY(3, 3)
 
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
-int glds_num_cfgs() { return kNumGlds + halo_num_cfgs(); }
+int glds_num_cfgs() { return kNumGlds + halo_num_cfgs() + resident_num_cfgs(); }
 
-bool glds_is_halo(int cfg) { return cfg >= kNumGlds; }
+// numbering: LDS-DMA configs, then halo configs, then the weight-stationary 1x1 configs
+static int res_base() { return kNumGlds + halo_num_cfgs(); }
+
+bool glds_is_halo(int cfg) { return cfg >= kNumGlds && cfg < res_base(); }
+
+bool glds_is_resident(int cfg) { return cfg >= res_base(); }
 
 int glds_cfg_bk(int cfg) { return cfg >= kNumGlds ? 64 : kGlds[cfg].bk; }
 
 // Same rules as launch_one / launch_glds (accumulator budget, K-step width, LDS per CU).
 bool glds_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs) {
+  if (cfg >= res_base()) return resident_supported(cfg - res_base(), cin, cout, kh, kw, limbs, wlimbs);
   if (cfg >= kNumGlds) return halo_supported(cfg - kNumGlds, cin, cout, kh, kw, limbs, wlimbs);
   const GldsCfg& c = kGlds[cfg];
   if (cin % 64 != 0 || cout % 16 != 0 || (c.bk == 128 && cin % 128 != 0)) return false;
@@ -62,6 +68,7 @@ int glds_default_cfg(const ConvArgs& a, int limbs, int wlimbs) {
 }
 
 void glds_cfg_info(int cfg, int* bm, int* bn, int* threads) {
+  if (cfg >= res_base()) return resident_cfg_info(cfg - res_base(), bm, bn, threads);
   if (cfg >= kNumGlds) return halo_cfg_info(cfg - kNumGlds, bm, bn, threads);
   const GldsCfg& c = kGlds[cfg];
   *bm = 16 * c.wp * c.wavesp;  // pixels (GEMM rows)
@@ -86,6 +93,7 @@ int launch_glds(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s
   if ((!a.s2d && a.cin % kKStep != 0) || a.cout % 16 != 0 || !glds_planes_ok(a, limbs, wlimbs))
     return fail(SMPQ_E_INVALID,
                 "smpq_conv2d_fwd: LDS-DMA tile configs need cin % 64 == 0, cout % 16 == 0 and planes < 2 GiB");
+  if (cfg >= res_base()) return launch_resident(cfg - res_base(), limbs, wlimbs, a, s);
   if (cfg >= kNumGlds) return launch_halo(cfg - kNumGlds, limbs, wlimbs, a, s);
   if (a.s2d) {
     if (wlimbs == 2 && limbs == 1) return launch_s2d<1, 2>(cfg, a, s);

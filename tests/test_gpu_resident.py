@@ -1,0 +1,105 @@
+"""Weight-stationary 1x1 tiles (csrc/conv_resident.hip, tile kind TILE_RESIDENT1X1): their
+static-range limb-plane outputs and overflow flags equal the LDS-DMA kernel's bit for bit — 24-bit
+fixed-point (3-limb) weights as in the downsample convs and exact codes (1 limb), with and without
+ReLU, stride 1 and 2, partial last tiles, several tiles per workgroup, in range and overflowing —
+and the calls they do not run are refused before launching. Every call goes through the C-ABI."""
+import pytest
+import torch
+
+from test_gpu import make_layer
+
+pytestmark = pytest.mark.gpu
+
+
+def _res_cfgs(ops):
+    return [c for c in ops.tile_configs() if ops.tile_kind(c) == ops.TILE_RESIDENT1X1]
+
+
+def _layer(gpu, wl, seed):
+    from smpq import ops
+    if wl == 1:
+        wd, step, codes, offset = make_layer(gpu, 64, 256, 1, seed=seed, bits_choice=(6, 4))
+        return codes, None, step
+    g = torch.Generator().manual_seed(seed)
+    w = (torch.randn(256, 64, 1, 1, generator=g) * 0.1).to(gpu)
+    codes, offset, wscale, st = ops.pack_weights_ex(w, None, 3)
+    return codes, None, wscale
+
+
+@pytest.mark.parametrize("wl", [3, 1])
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("n,h,stride", [(3, 56, 1), (2, 13, 1), (1, 5, 1), (2, 28, 2), (5, 9, 2)])
+def test_resident_equals_lds_dma(gpu, wl, relu, n, h, stride):
+    from smpq import ops
+    cfgs = _res_cfgs(ops)
+    assert len(cfgs) == 2
+    codes, offset, scale = _layer(gpu, wl, seed=7 * n + h + wl)
+    g = torch.Generator().manual_seed(h + 11 * n)
+    x = torch.relu(torch.randn(n, h, h, 64, generator=g)).to(gpu)
+    x[0] *= 3.0
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, 3)
+    shift = torch.linspace(-0.5, 0.5, 256, device=gpu)
+    ref = ops.conv2d_q(xq, am, codes, offset, 1, 1, stride, 0, scale, shift, relu=relu)
+    for frac in (2.0, 0.4):
+        rng = float(ref.abs().max()) * frac
+        ovf0 = torch.zeros(1, dtype=torch.int32, device=gpu)
+        _, yq0 = ops.conv2d_q(xq, am, codes, offset, 1, 1, stride, 0, scale, shift, relu=relu, tile_cfg=-1,
+                              emit_range=rng, overflow=ovf0, want_f32=False)
+        assert int(ovf0.item()) == (1 if frac < 1 else 0)
+        for c in cfgs:
+            for _ in range(3):  # repeated launches: no race between a tile's DMA and the last one's reads
+                ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+                _, yq = ops.conv2d_q(xq, am, codes, offset, 1, 1, stride, 0, scale, shift, relu=relu, tile_cfg=c,
+                                     emit_range=rng, overflow=ovf, want_f32=False)
+                assert torch.equal(yq, yq0), (c, frac)
+                assert torch.equal(ovf, ovf0), (c, frac)
+
+
+def test_resident_many_tiles_per_workgroup(gpu):
+    """More tiles than resident workgroups (each walks ~25 tiles), the R50 downsample's shape at a
+    quarter of the batch: bitwise the LDS-DMA kernel's limb planes."""
+    from smpq import ops
+    codes, offset, scale = _layer(gpu, 3, seed=5)
+    x = torch.relu(torch.randn(64, 56, 56, 64, generator=torch.Generator().manual_seed(9))).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, 3)
+    shift = torch.linspace(-0.1, 0.1, 256, device=gpu)
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+    _, yq0 = ops.conv2d_q(xq, am, codes, offset, 1, 1, 1, 0, scale, shift, tile_cfg=-1, emit_range=8.0,
+                          overflow=ovf, want_f32=False)
+    for c in _res_cfgs(ops):
+        _, yq = ops.conv2d_q(xq, am, codes, offset, 1, 1, 1, 0, scale, shift, tile_cfg=c, emit_range=8.0,
+                             overflow=ovf, want_f32=False)
+        assert torch.equal(yq, yq0), c
+    assert int(ovf.item()) == 0
+
+
+def test_resident_refuses_what_it_does_not_run(gpu):
+    """fp32 outputs, a residual, weight offsets, pad > 0 and other shapes: SMPQ_E_INVALID before
+    launching (the autotuner skips such calls); tile_supported reports the shape rule."""
+    from smpq import _lib, ops
+    c = _res_cfgs(ops)[0]
+    assert ops._tile_fits(c, 3, 3, 256, 64, 1) and ops._tile_fits(c, 3, 1, 256, 64, 1)
+    assert not ops._tile_fits(c, 3, 1, 128, 64, 1) and not ops._tile_fits(c, 3, 1, 256, 128, 1)
+    assert not ops._tile_fits(c, 2, 1, 256, 64, 1) and not ops._tile_fits(c, 3, 1, 256, 64, 3)
+    codes, offset, scale = _layer(gpu, 1, seed=3)
+    x = torch.relu(torch.randn(1, 8, 8, 64, generator=torch.Generator().manual_seed(2))).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, 3)
+    shift = torch.zeros(256, device=gpu)
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+    with pytest.raises(_lib.SmpqError, match="resident"):  # fp32 output
+        ops.conv2d_q(xq, am, codes, offset, 1, 1, 1, 0, scale, shift, tile_cfg=c)
+    rq = ops.act_quantize(torch.relu(torch.randn(1, 8, 8, 256, device=gpu)), torch.full((1,), 4.0, device=gpu), 3)
+    with pytest.raises(_lib.SmpqError, match="resident"):  # limb-plane residual
+        ops.conv2d_q(xq, am, codes, offset, 1, 1, 1, 0, scale, shift, tile_cfg=c, emit_range=1.0, overflow=ovf,
+                     want_f32=False, residual_q=rq, residual_range=4.0)
+    with pytest.raises(_lib.SmpqError, match="resident"):  # pad 1
+        ops.conv2d_q(xq, am, codes, offset, 1, 1, 1, 1, scale, shift, tile_cfg=c, emit_range=1.0, overflow=ovf,
+                     want_f32=False)
+    off = torch.zeros(256, dtype=torch.int32, device=gpu)
+    off[3] = 5
+    with pytest.raises(_lib.SmpqError, match="resident"):  # weight offsets
+        ops.conv2d_q(xq, am, codes, off, 1, 1, 1, 0, scale, shift, tile_cfg=c, emit_range=1.0, overflow=ovf,
+                     want_f32=False)

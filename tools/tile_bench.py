@@ -48,7 +48,7 @@ for name, cin, cout, k, s, h, res, wl in SHAPES:
     _, ref = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, wscale, shift, tile_cfg=-1, **kw)
     out = []
     for c in ops.tile_configs():
-        if ops.tile_kind(c) not in (ops.TILE_LDS_DMA, ops.TILE_LDS_DMA_K128, ops.TILE_HALO3X3):
+        if ops.tile_kind(c) not in (ops.TILE_LDS_DMA, ops.TILE_LDS_DMA_K128, ops.TILE_HALO3X3, ops.TILE_RESIDENT1X1):
             continue
         if not ops._tile_fits(c, L, wl, cout, cin, k) or (CFGS is not None and c not in CFGS):
             continue
