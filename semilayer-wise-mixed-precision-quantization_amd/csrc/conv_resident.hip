@@ -1,19 +1,27 @@
-// Weight-stationary 1x1 conv tiles for gfx950 (round 6; tile kind SMPQ_TILE_RESIDENT1X1): the
-// 1x1 convs with ONE 64-wide K step and 256 output channels whose epilogue only emits the next
-// conv's limb planes — in the R50 forward the downsample of layer1[0] (resnet.py:188-192: conv1x1
-// 64 -> 256 + BN, 24-bit fixed-point weights, 6 MFMA passes) — where the LDS-DMA kernel spends most
-// of its staging on the weights: a 128 x 32 tile re-stages 24 KB of weight limbs for 6 KB of
-// activations, 50,176 times per 256 images.
+// Weight-stationary 1x1 conv tiles for gfx950 (round 6; tile kind SMPQ_TILE_RESIDENT1X1): 1x1 convs
+// whose epilogue only emits the next conv's limb planes (optionally adding a limb-plane residual)
+// and whose weights — for a slab of output channels — fit in the VGPRs of a workgroup. In the R50
+// forward: the 1x1 convs of the Bottlenecks and the four downsample convs
+// (resnet.py:188-192, conv1x1 + BN, 24-bit fixed-point weights: 3 weight limbs, 6 MFMA passes),
+// where the LDS-DMA kernel spends most of its operand staging on the weights (a 128 x 32 tile of
+// the 64 -> 256 downsample re-stages 24 KB of weight limbs for 6 KB of activations, 50,176 times per
+// 256 images; the strided 256 -> 512 / 512 -> 1024 ones 3 bytes of weights per K element and output
+// channel).
 //
-// Here a persistent workgroup (4 waves, wave w = output channels 64 w .. 64 w + 63) loads every
-// weight limb ONCE, straight into VGPRs (LW x 4 A fragments per wave: each lane's 16 bytes are one
-// buffer load), and walks pixel tiles of BP pixels (tile b, b + grid, b + 2 grid, ...): the activation tile of
-// tile t + 1 is DMA'd into the other of two LDS stages while tile t's MFMAs and epilogue run; the
-// epilogue is the lean static-range epilogue of the LDS-DMA kernel (lean_quad: limb recombination,
-// folded BN, optional ReLU, rounding, clamp, digit encode), staged in LDS as a [L][BP][256] tile and
-// copied out as whole 256-B pixel rows. Integer accumulation is exact and the epilogue is the same
-// function, so the outputs and the overflow flag are bitwise those of every other tile config
-// (tests/test_gpu_resident.py).
+// A persistent workgroup (4 waves) owns one slab of BN = 64 CW output channels (wave w: channels
+// 16 CW w .. 16 CW (w + 1) - 1 of the slab) and loads the slab's weight limbs for the whole K ONCE,
+// straight into VGPRs (LW x KC x CW A fragments per wave: each lane's 16 bytes are one buffer load).
+// It then walks pixel tiles of BP pixels (tiles t0, t0 + stride, ...): the activation tile of the
+// next tile ([L][BP][K] bytes, K = 64 KC, rows swizzled by 16-B chunk) arrives by LDS-DMA into the
+// other of two stages while this tile's MFMAs and epilogue run. The epilogue is the LDS-DMA kernel's
+// lean static-range epilogue (lean_quad: limb recombination, folded BN, optional ReLU, rounding,
+// clamp, digit encode), staged in LDS as a [L][BP][BN] tile and copied out row-major. Integer
+// accumulation is exact and the epilogue is the same function, so the outputs and the overflow flag
+// are bitwise those of every other tile config (tests/test_gpu_resident.py). A limb-plane residual
+// (conv3 + the block input, resnet.py:111-113) arrives by LDS-DMA with the activations, one tile
+// ahead, as a [L][BP][BN] tile in the output tile's layout. The slabs of a conv
+// walk the same pixel tiles in the same order, so a tile's activations are read from HBM once and
+// from L2 / MALL by the other slabs.
 #include "conv_common.h"
 #include "lds_dma.h"
 
@@ -22,150 +30,223 @@ namespace smpq {
 namespace {
 
 struct ResCfg {
-  int bp;  // pixels per tile (16 x WP)
+  int cw, wp;   // 16-channel fragments per wave (slab = 64 cw channels), 16-pixel fragments per tile
+  int kc_mask;  // bit k: K = 64 k supported (chunks of 64 bytes per activation row)
 };
-constexpr ResCfg kRes[] = {{32}, {16}};
+constexpr ResCfg kRes[] = {
+    {4, 2, 1 << 1},                                // 0: slab 256, 32 px, K 64 (the 64 -> 256 downsample)
+    {4, 1, (1 << 1) | (1 << 2) | (1 << 4)},        // 1: slab 256, 16 px, K 64..256 (the expansions)
+    {1, 1, 0x10116},                               // 2: slab 64, 16 px, K 64..1024 (strided ds, reductions)
+    {2, 1, 0x10116},                               // 3: slab 128, 16 px, K 64..1024
+    // (slab 64 x 32 px at K 256 / 512 measured 1.1-2.1x slower than 16 px: one workgroup per CU)
+};
+// the weight fragments a wave holds: at most 32 (128 VGPRs)
+constexpr bool res_fits(int lw, int kc, int cw) { return lw * kc * cw <= 32; }
 constexpr int kNumRes = sizeof(kRes) / sizeof(kRes[0]);
-constexpr int kResCout = 256;  // output channels (all of them per workgroup: 4 waves x 64)
 constexpr int kResThreads = 256;
 
-// MINW: workgroups per CU the register budget is compiled for (one wave per SIMD each)
-template <int L, int LW, int WP, bool RELU, int MINW>
-__global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvArgs a, int ntiles) {
-  constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
-  constexpr int NACC = L + LW - 1 - SMIN;
-  constexpr int WC = 4;                       // 16-channel blocks per wave
-  constexpr int BP = 16 * WP;                 // pixels per tile
-  constexpr int ASTAGE = L * BP * 64;         // activation tile bytes
-  constexpr int APIECES = L * BP / 16;        // 1-KiB DMA pieces per activation tile
-  constexpr int OTILE = L * BP * kResCout;    // staged output tile bytes
+// the 16-B chunk c of activation row r is stored at chunk ach<KC>(c, r): conflict-free DMA writes and
+// fragment reads (16 rows, chunk fixed per lane group) for 64-B rows (KC = 1, the LDS-DMA kernel's
+// swizzle) and for rows of 16 or more chunks (KC >= 4: XOR by the row's low 4 bits)
+template <int KC>
+__device__ __forceinline__ int ach(int c, int r) {
+  if constexpr (KC == 1) return c ^ swz<64>(r & 15);
+  else if constexpr (KC == 2) return c ^ swz<128>(r);
+  else return c ^ (r & 15);
+}
+
+template <int L, int LW, int KC, int CW, int WP, bool RES>
+struct ResShape {
+  static constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
+  static constexpr int NACC = L + LW - 1 - SMIN;
+  static constexpr int BN = 64 * CW, BP = 16 * WP, K = 64 * KC;
+  static constexpr int ASTAGE = L * BP * K;  // activation tile bytes
+  static constexpr int OTILE = L * BP * BN;  // output (and residual) tile bytes
+  static constexpr int LDS = 2 * ASTAGE + (RES ? 3 : 1) * OTILE;
+  // VGPRs: weights + accumulators + one chunk's B fragments + addressing / epilogue (~40)
+  static constexpr int REGS = 4 * (LW * KC * CW + NACC * CW * WP + L * WP) + 40;
+  static constexpr int MINW_R = REGS <= 128 ? 4 : (REGS <= 160 ? 3 : 2);  // workgroups per CU (1 wave per SIMD each)
+  static constexpr int MINW_L = (160 * 1024) / LDS;
+  static constexpr int MINW = MINW_R < MINW_L ? MINW_R : MINW_L;
+};
+
+template <int L, int LW, int KC, int CW, int WP, bool RELU, bool RES, int MINW>
+__global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvArgs a, int ntiles, int nslabs) {
+  using S = ResShape<L, LW, KC, CW, WP, RES>;
+  constexpr int SMIN = S::SMIN, NACC = S::NACC, BN = S::BN, BP = S::BP, K = S::K, ASTAGE = S::ASTAGE;
+  constexpr int CH = K / 16;       // 16-B chunks per activation row
+  constexpr int RP = 1024 / K;     // activation rows per 1-KiB DMA piece
+  constexpr int APIECES = L * BP / RP;
   constexpr float qmax = act_qmax<L>();
-  extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // 2 activation stages + the output tile
+  extern __shared__ __attribute__((aligned(1024))) int8_t lds[];  // 2 act stages, output tile, 2 residual tiles
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int frow = lane & 15;
-  const int rd = frow * 64 + 16 * ((lane >> 4) ^ swz<64>(frow));  // fragment read offset in a 16-row block
+  const int frow = lane & 15, grp = lane >> 4;
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
-  int8_t* const astage = lds;
   int8_t* const otile = lds + 2 * ASTAGE;
+  constexpr int OTILE = S::OTILE;
+  const unsigned rtile0 = lds0 + 2 * ASTAGE + OTILE;  // residual tile of stage s at rtile0 + s OTILE
+  const int slab = blockIdx.x % nslabs;
+  const int n0 = slab * BN;
+  const int tstride = gridDim.x / nslabs;
 
-  // ---- the weight limbs -> VGPRs once: A fragment (lw, i) of lane (g, p) = the 16 bytes of K chunk
-  // g of output channel 16 (4 wave + i) + p (row-major [LW][256][64] = the K-major layout at K 64)
+  // ---- the slab's weight limbs -> VGPRs once: A fragment (lw, kc, i) of lane (g, p) = the 16
+  // bytes of K chunk 4 kc + g of output channel n0 + 16 (CW wave + i) + p
   const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.codes), 0, (int)(LW * a.wplane), 0x00020000);
-  v4i wa[LW][WC];
+  v4i wa[LW][KC][CW];
 #pragma unroll
   for (int lw = 0; lw < LW; ++lw)
 #pragma unroll
-    for (int i = 0; i < WC; ++i) {
-      const v4u v = __builtin_amdgcn_raw_buffer_load_b128(
-          wrs, (unsigned)(((wave * WC + i) * 16 + frow) * 64 + 16 * (lane >> 4)), (unsigned)(lw * a.wplane), 0);
-      wa[lw][i] = v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
-    }
-  const int prow = lane >> 2;                        // row inside a 1-KiB DMA piece
-  const int pchunk = (lane & 3) ^ swz<64>(prow);     // logical K chunk this lane fetches
-  // per-lane activation source: pixel m's 64 channels (1x1, any stride) of limb l
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+      for (int i = 0; i < CW; ++i) {
+        const int row = n0 + (wave * CW + i) * 16 + frow;
+        const unsigned off = a.w_kmajor ? (unsigned)(kc * a.cout * 64 + row * 64 + 16 * grp)
+                                        : (unsigned)(row * K + kc * 64 + 16 * grp);
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(wrs, off, (unsigned)(lw * a.wplane), 0);
+        wa[lw][kc][i] = v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+      }
+
+  // ---- activation DMA: piece = RP pixel rows x K bytes of one limb; lane -> (row, physical chunk)
+  const int prow = lane / CH, pphys = lane % CH;
   const v4i xrs = make_rsrc(a.xq, (long long)L * a.plane);
   const int hw_out = a.ho * a.wo;
-  auto act_src = [&](int m) -> unsigned {  // byte offset of pixel m's channel chunk pchunk in plane 0
-    if (m >= a.M) return kOOB;
-    const int img = fast_div(m, a.hw_mul, a.hw_shr);
-    const int rem = m - img * hw_out;
-    const int oh = fast_div(rem, a.wo_mul, a.wo_shr), ow = rem - oh * a.wo;
-    return (unsigned)(((img * a.h + oh * a.stride) * a.w + ow * a.stride) * 64 + 16 * pchunk);
-  };
-  auto issue_acts = [&](int t, int stage) {  // this wave's pieces of tile t's activation tile
+  auto issue_acts = [&](int t, int stage) {
     for (int p = wave; p < APIECES; p += 4) {
-      const int l = p / (BP / 16), rb = (p % (BP / 16)) * 16;
-      const unsigned src = act_src(t * BP + rb + prow);
-      dma16(lds0 + stage * ASTAGE + p * 1024, xrs, src,
-            __builtin_amdgcn_readfirstlane((unsigned)((long long)l * a.plane)));
+      const int l = p / (BP / RP), r = (p % (BP / RP)) * RP + prow;  // tile row (pixel) of this lane
+      const int m = t * BP + r;
+      unsigned src = kOOB;
+      if (m < a.M) {
+        const int img = fast_div(m, a.hw_mul, a.hw_shr);
+        const int rem = m - img * hw_out;
+        const int oh = fast_div(rem, a.wo_mul, a.wo_shr), ow = rem - oh * a.wo;
+        src = (unsigned)(((img * a.h + oh * a.stride) * a.w + ow * a.stride) * K + 16 * ach<KC>(pphys, r));
+      }
+      dma16(lds0 + stage * ASTAGE + p * 1024, xrs, src, __builtin_amdgcn_readfirstlane((unsigned)((long long)l * a.plane)));
     }
   };
-  int t = blockIdx.x;
-  if (t < ntiles) issue_acts(t, 0);
+  // the residual tile [L][BP][BN] of tile t (RES): piece = 1024 / BN rows x BN bytes of one limb, 16-B
+  // chunk c of tile row r at c ^ swze<BN>(r & 15) (the output tile's layout: the epilogue reads it
+  // with the same addressing)
+  const long long oplane = (long long)a.M * a.cout;
+  const v4i rrs = make_rsrc(a.res_q, RES ? (long long)L * oplane : 0);
+  auto issue_res = [&](int t, int stage) {
+    if constexpr (RES) {
+      constexpr int RROWS = 1024 / BN, RCPR = BN / 16, RPIECES = L * BP / RROWS;
+      const int rrow = lane / RCPR, rpc = lane % RCPR;
+      for (int p = wave; p < RPIECES; p += 4) {
+        const int l = p / (BP / RROWS), rt = (p % (BP / RROWS)) * RROWS + rrow;
+        const int m = t * BP + rt;
+        const unsigned src = m < a.M ? (unsigned)((long long)m * a.cout + n0 + 16 * (rpc ^ swze<BN>(rt & 15))) : kOOB;
+        dma16(rtile0 + stage * OTILE + p * 1024, rrs, src, __builtin_amdgcn_readfirstlane((unsigned)((long long)l * oplane)));
+      }
+    }
+  };
+  int t = blockIdx.x / nslabs;
+  if (t < ntiles) {
+    issue_acts(t, 0);
+    issue_res(t, 0);
+  }
 
   // ---- epilogue constants of this lane's channels -----------------------------------------------
   const float inv = a.yq_inv;
-  float csq[WC][4], shq[WC][4];
+  float csq[CW][4], shq[CW][4];
 #pragma unroll
-  for (int i = 0; i < WC; ++i) {
-    const int c = (wave * WC + i) * 16 + 4 * (lane >> 4);
+  for (int i = 0; i < CW; ++i) {
+    const int c = n0 + (wave * CW + i) * 16 + 4 * grp;
     const float4 cs = *reinterpret_cast<const float4*>(a.col_scale + c);
     const float4 csh = *reinterpret_cast<const float4*>(a.col_shift + c);
     csq[i][0] = cs.x * inv, csq[i][1] = cs.y * inv, csq[i][2] = cs.z * inv, csq[i][3] = cs.w * inv;
     shq[i][0] = csh.x * inv, shq[i][1] = csh.y * inv, shq[i][2] = csh.z * inv, shq[i][3] = csh.w * inv;
   }
   const float lo = RELU ? 0.f : -qmax;
-  const long long oplane = (long long)a.M * kResCout;
+  const float rsq = a.res_scale * inv;
   const v4i qrs4 = make_rsrc(a.yq, (long long)L * oplane);
   const bool nt = __builtin_amdgcn_readfirstlane(a.nt_store) != 0;
   float vmax = 0.f;
 
   int stage = 0;
-  for (; t < ntiles; t += gridDim.x) {
+  for (; t < ntiles; t += tstride) {
     const int m0 = t * BP;
-    // tile t's activations have landed (this wave's pieces; the barrier: every wave's), and every
-    // wave is past the previous tile's copy-out, so the output tile may be rewritten below
+    // tile t's activations have landed (this wave's pieces; after the barrier every wave's), and
+    // every wave is past the previous tile's copy-out and its reads of the other stage
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    v4i fb[L][WP];
-#pragma unroll
-    for (int l = 0; l < L; ++l)
-#pragma unroll
-      for (int j = 0; j < WP; ++j)
-        fb[l][j] = *reinterpret_cast<const v4i*>(astage + stage * ASTAGE + (l * BP + j * 16) * 64 + rd);
-    if (t + (int)gridDim.x < ntiles) issue_acts(t + gridDim.x, stage ^ 1);  // under this tile's work
-    v4i acc[NACC][WC][WP];
+    if (t + tstride < ntiles) {  // under this tile's work
+      issue_acts(t + tstride, stage ^ 1);
+      issue_res(t + tstride, stage ^ 1);
+    }
+    const int8_t* as = lds + stage * ASTAGE;
+    v4i acc[NACC][CW][WP];
 #pragma unroll
     for (int s = 0; s < NACC; ++s)
 #pragma unroll
-      for (int i = 0; i < WC; ++i)
+      for (int i = 0; i < CW; ++i)
 #pragma unroll
         for (int j = 0; j < WP; ++j) acc[s][i][j] = v4i{0, 0, 0, 0};
 #pragma unroll
-    for (int l = 0; l < L; ++l)
+    for (int kc = 0; kc < KC; ++kc) {
+      v4i fb[L][WP];
 #pragma unroll
-      for (int lw = 0; lw < LW; ++lw) {
-        if (l + lw < SMIN) continue;  // compile-time: skipped low-digit product (as the LDS-DMA kernel)
+      for (int l = 0; l < L; ++l)
 #pragma unroll
-        for (int i = 0; i < WC; ++i)
+        for (int j = 0; j < WP; ++j) {
+          const int r = j * 16 + frow;
+          fb[l][j] = *reinterpret_cast<const v4i*>(as + (l * BP + r) * K + 16 * ach<KC>(4 * kc + grp, r));
+        }
 #pragma unroll
-          for (int j = 0; j < WP; ++j)
-            acc[l + lw - SMIN][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wa[lw][i], fb[l][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
-      }
-    // lean epilogue -> the [L][BP][256] output tile in LDS (row = pixel, 16-B chunk c of a row at
-    // c ^ swze<256>(row & 15): conflict-free, as the LDS-DMA kernel's staged tiles)
+      for (int l = 0; l < L; ++l)
+#pragma unroll
+        for (int lw = 0; lw < LW; ++lw) {
+          if (l + lw < SMIN) continue;  // compile-time: skipped low-digit product (as the LDS-DMA kernel)
+#pragma unroll
+          for (int i = 0; i < CW; ++i)
+#pragma unroll
+            for (int j = 0; j < WP; ++j)
+              acc[l + lw - SMIN][i][j] =
+                  __builtin_amdgcn_mfma_i32_16x16x64_i8(wa[lw][kc][i], fb[l][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
+        }
+    }
+    // lean epilogue -> the [L][BP][BN] output tile in LDS (16-B chunk c of tile row r at
+    // c ^ swze<BN>(r & 15), as the LDS-DMA kernel's staged tiles)
 #pragma unroll
     for (int j = 0; j < WP; ++j) {
       const int m = m0 + j * 16 + frow;
       const float rscale = m < a.M ? a.x_absmax[fast_div(m, a.hw_mul, a.hw_shr)] * a.inv_qmax : 0.f;
 #pragma unroll
-      for (int i = 0; i < WC; ++i) {
+      for (int i = 0; i < CW; ++i) {
         v4i accq[NACC];
 #pragma unroll
         for (int s = 0; s < NACC; ++s) accq[s] = acc[s][i][j];
+        const int rt = j * 16 + frow, cc = wave * CW + i;
+        int rqv[4] = {0, 0, 0, 0};
+        if constexpr (RES) {
+          unsigned rw[L];
+#pragma unroll
+          for (int l = 0; l < L; ++l)
+            rw[l] = *reinterpret_cast<const unsigned*>(lds + 2 * ASTAGE + (1 + stage) * OTILE + l * BP * BN + rt * BN +
+                                                       16 * (cc ^ swze<BN>(frow)) + 4 * grp);
+          decode4<L>(rw, rqv);
+        }
         unsigned wq[L];
-        const float mm = lean_quad<L, NACC, SMIN>(accq, rscale, csq[i], shq[i], false, nullptr, 0.f, RELU, lo, wq);
+        const float mm = lean_quad<L, NACC, SMIN>(accq, rscale, csq[i], shq[i], RES, rqv, rsq, RELU, lo, wq);
         vmax = m < a.M ? fmaxf(vmax, mm) : vmax;
-        const int rt = j * 16 + frow, cc = wave * WC + i;
 #pragma unroll
         for (int l = 0; l < L; ++l)
-          *reinterpret_cast<unsigned*>(otile + l * BP * kResCout + rt * kResCout + 16 * (cc ^ swze<kResCout>(frow)) +
-                                       4 * (lane >> 4)) = wq[l];
+          *reinterpret_cast<unsigned*>(otile + l * BP * BN + rt * BN + 16 * (cc ^ swze<BN>(frow)) + 4 * grp) = wq[l];
       }
     }
     __syncthreads();
-    // copy-out: whole 256-B pixel rows, 16 B per lane
-    constexpr int ITEMS = OTILE / 16;
+    // copy-out: BN-byte pixel rows of the slab, 16 B per lane
+    constexpr int RC = BN / 16, ITEMS = L * BP * RC;
 #pragma unroll
     for (int k = 0; k < (ITEMS + kResThreads - 1) / kResThreads; ++k) {
       const int it = threadIdx.x + kResThreads * k;
       if (ITEMS % kResThreads == 0 || it < ITEMS) {
-        const int l = it / (BP * 16), rem = it - l * (BP * 16);
-        const int rt = rem >> 4, c = rem & 15;
-        const v4i v = *reinterpret_cast<const v4i*>(otile + l * BP * kResCout + rt * kResCout +
-                                                     16 * (c ^ swze<kResCout>(rt & 15)));
-        const unsigned off = m0 + rt < a.M ? (unsigned)((long long)(m0 + rt) * kResCout + 16 * c) : kOOB;
+        const int l = it / (BP * RC), rem = it - l * (BP * RC);
+        const int rt = rem / RC, c = rem - rt * RC;
+        const v4i v = *reinterpret_cast<const v4i*>(otile + l * BP * BN + rt * BN + 16 * (c ^ swze<BN>(rt & 15)));
+        const unsigned off = m0 + rt < a.M ? (unsigned)((long long)(m0 + rt) * a.cout + n0 + 16 * c) : kOOB;
         store_limbs16(v4u{(unsigned)v.x, (unsigned)v.y, (unsigned)v.z, (unsigned)v.w}, qrs4, off,
                       __builtin_amdgcn_readfirstlane((unsigned)((long long)l * oplane)), nt);
       }
@@ -187,34 +268,57 @@ int device_cus_res() {
   return cus;
 }
 
-template <int L, int LW, int WP, bool RELU>
+template <int L, int LW, int CFG, int KC, bool RELU, bool RES>
 int launch_res_one(const ConvArgs& a, hipStream_t s) {
-  constexpr int BP = 16 * WP;
-  constexpr int lds_bytes = 2 * L * BP * 64 + L * BP * kResCout;
-  // the register budget (one wave per SIMD per workgroup): 3 workgroups per CU where the
-  // accumulators allow it (<= 168 VGPRs), else 2
-  constexpr int MINW = (L + LW - 1 - ((L + LW - 4) > 0 ? (L + LW - 4) : 0)) * 4 * WP * 4 <= 48 ? 3 : 2;
-  static_assert(MINW * lds_bytes <= 160 * 1024, "LDS per CU");
-  auto k = qconv_resident_kernel<L, LW, WP, RELU, MINW>;
+  constexpr int CW = kRes[CFG].cw, WP = kRes[CFG].wp;
+  if constexpr (!((kRes[CFG].kc_mask >> KC) & 1) || !res_fits(LW, KC, CW)) {
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tile: cin not built for this configuration");
+  } else {
+  using S = ResShape<L, LW, KC, CW, WP, RES>;
+  static_assert(S::MINW >= 1, "LDS per CU");
+  auto k = qconv_resident_kernel<L, LW, KC, CW, WP, RELU, RES, S::MINW>;
   static const hipError_t attr = [&] {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
     if (e != hipSuccess) (void)hipGetLastError();
     return e;
   }();
   if (attr != hipSuccess) return check_hip(attr, "qconv_resident_kernel LDS attribute");
-  const long long ntiles = ((long long)a.M + BP - 1) / BP;
+  const long long ntiles = ((long long)a.M + S::BP - 1) / S::BP;
+  const int nslabs = a.cout / S::BN;
   if (ntiles > 0x7fffffffLL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
-  // persistent: as many workgroups as fit the CUs at once, at most one per tile
-  long long blocks = (long long)device_cus_res() * MINW;
-  if (blocks > ntiles) blocks = ntiles;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kResThreads), lds_bytes, s, a, (int)ntiles);
+  // persistent: as many workgroups as fit the CUs at once, a multiple of the slab count (every slab
+  // walks the tiles with the same stride), at most one per (slab, tile)
+  long long per_slab = (long long)device_cus_res() * S::MINW / nslabs;
+  if (per_slab < 1) per_slab = 1;
+  if (per_slab > ntiles) per_slab = ntiles;
+  const long long blocks = per_slab * nslabs;
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kResThreads), S::LDS, s, a, (int)ntiles, nslabs);
   return check_hip(hipGetLastError(), "qconv_resident_kernel launch");
+  }
 }
 
-template <int L, int LW, bool RELU>
+template <int L, int LW, int CFG, bool RELU, bool RES>
+int launch_res_kc(int kc, const ConvArgs& a, hipStream_t s) {
+  switch (kc) {  // only the K sizes of the configuration's mask are instantiated
+    case 1: return launch_res_one<L, LW, CFG, 1, RELU, RES>(a, s);
+    case 2: return launch_res_one<L, LW, CFG, 2, RELU, RES>(a, s);
+    case 4: return launch_res_one<L, LW, CFG, 4, RELU, RES>(a, s);
+    case 8: return launch_res_one<L, LW, CFG, 8, RELU, RES>(a, s);
+    case 16: return launch_res_one<L, LW, CFG, 16, RELU, RES>(a, s);
+    default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tile: cin not built");
+  }
+}
+
+template <int L, int LW, bool RELU, bool RES>
 int launch_res_l(int cfg, const ConvArgs& a, hipStream_t s) {
-  return kRes[cfg].bp == 16 ? launch_res_one<L, LW, 1, RELU>(a, s) : launch_res_one<L, LW, 2, RELU>(a, s);
+  const int kc = a.cin / 64;
+  switch (cfg) {
+    case 0: return launch_res_kc<L, LW, 0, RELU, RES>(kc, a, s);
+    case 1: return launch_res_kc<L, LW, 1, RELU, RES>(kc, a, s);
+    case 2: return launch_res_kc<L, LW, 2, RELU, RES>(kc, a, s);
+    default: return launch_res_kc<L, LW, 3, RELU, RES>(kc, a, s);
+  }
 }
 
 }  // namespace
@@ -222,27 +326,39 @@ int launch_res_l(int cfg, const ConvArgs& a, hipStream_t s) {
 int resident_num_cfgs() { return kNumRes; }
 
 void resident_cfg_info(int cfg, int* bm, int* bn, int* threads) {
-  *bm = kRes[cfg].bp;
-  *bn = kResCout;
+  *bm = 16 * kRes[cfg].wp;
+  *bn = 64 * kRes[cfg].cw;
   *threads = kResThreads;
 }
 
 // What tile_supported can see; the launcher also needs pad 0, no weight offsets and the
 // static-range limb-plane epilogue without a residual (yq set; y, y_absmax, residual, residual_q NULL).
 bool resident_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs) {
-  if (cfg < 0 || cfg >= kNumRes) return false;
-  return kh == 1 && kw == 1 && cin == 64 && cout == kResCout && limbs == 3 && (wlimbs == 1 || wlimbs == 3);
+  if (cfg < 0 || cfg >= kNumRes || kh != 1 || kw != 1 || limbs != 3 || !(wlimbs == 1 || wlimbs == 3)) return false;
+  const ResCfg& c = kRes[cfg];
+  return cin % 64 == 0 && cin / 64 < 31 && ((c.kc_mask >> (cin / 64)) & 1) && cout % (64 * c.cw) == 0 &&
+         res_fits(wlimbs, cin / 64, c.cw);
 }
 
 int launch_resident(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s) {
   if (!resident_supported(cfg, a.cin, a.cout, a.kh, a.kw, limbs, wlimbs) || a.pad != 0 || a.s2d)
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tiles take 1x1 / pad 0 convs with cin 64, cout 256, "
-                                "3 activation limbs and 1 or 3 weight limbs");
-  if (!a.yq || a.y || a.residual || a.res_q || a.y_absmax || a.has_offset)
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tiles run the static-range limb-plane epilogue without "
-                                "a residual or weight offsets only");
-  if (wlimbs == 3) return a.relu ? launch_res_l<3, 3, true>(cfg, a, s) : launch_res_l<3, 3, false>(cfg, a, s);
-  return a.relu ? launch_res_l<3, 1, true>(cfg, a, s) : launch_res_l<3, 1, false>(cfg, a, s);
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tiles take 1x1 / pad 0 convs with 3 activation limbs, "
+                                "1 or 3 weight limbs and the tile's cin (64 .. 1024) and slab of couts");
+  if (!a.yq || a.y || a.residual || a.y_absmax || a.has_offset)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tiles run the static-range limb-plane epilogue (with a "
+                                "limb-plane residual or none) without weight offsets only");
+  // built variants: the downsamples (3 weight limbs, no ReLU, no residual), conv1 / conv2 (ReLU), conv3
+  // (ReLU + limb-plane residual) and plain (neither)
+  if (wlimbs == 3) {
+    if (a.relu || a.res_q)
+      return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tiles with 3 weight limbs: no ReLU or residual");
+    return launch_res_l<3, 3, false, false>(cfg, a, s);
+  }
+  if (a.res_q) {
+    if (!a.relu) return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tiles: a residual needs ReLU");
+    return launch_res_l<3, 1, true, true>(cfg, a, s);
+  }
+  return a.relu ? launch_res_l<3, 1, true, false>(cfg, a, s) : launch_res_l<3, 1, false, false>(cfg, a, s);
 }
 
 }  // namespace smpq

@@ -643,10 +643,12 @@ def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, 
     # now): the key does not carry relu / y_absmax, so other calls of a key never see them
     halo_ok = bool(relu and emit_range is not None and not want_f32 and residual is None and residual_q is None
                    and y_absmax is None and out is None and kh == 3 and kw == 3 and stride == 1 and pad == 1)
-    # the weight-stationary 1x1 tiles: the static-range limb-plane epilogue without a residual or
-    # weight offsets (cin 64 / cout 256 / 1x1 / pad 0: smpq_conv2d_tile_supported checks the shape)
-    res_ok = bool(emit_range is not None and not want_f32 and residual is None and residual_q is None
-                  and y_absmax is None and out is None and offset is None and kh == 1 and kw == 1 and pad == 0)
+    # the weight-stationary 1x1 tiles: the static-range limb-plane epilogue without weight offsets,
+    # built for the downsamples (3 weight limbs, no ReLU or residual) and for exact-code convs with
+    # ReLU + a limb-plane residual, ReLU only, or neither (smpq_conv2d_tile_supported checks the shape)
+    res_ok = bool(emit_range is not None and not want_f32 and residual is None and y_absmax is None
+                  and out is None and offset is None and kh == 1 and kw == 1 and pad == 0
+                  and (not (relu or residual_q is not None) if wlimbs == 3 else (relu or residual_q is None)))
     cands = [c for c in tile_configs() if _tile_fits(c, limbs, wlimbs, cout, cin, kh)
              and (halo_ok or tile_kind(c) != TILE_HALO3X3) and (res_ok or tile_kind(c) != TILE_RESIDENT1X1)]
     cfg = _choose_tile(key, run, cands, variant=None if (halo_ok or res_ok) else "nohalo")
