@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SMPQ_ABI_VERSION 6
+#define SMPQ_ABI_VERSION 7
 
 /* status codes */
 #define SMPQ_OK 0
@@ -199,6 +199,29 @@ int smpq_conv2d_fwd_q_km(const int8_t* xq, const float* x_absmax, int n, int h, 
                          float* y_absmax, int8_t* yq, float yq_range, int32_t* overflow,
                          const int8_t* residual_q, float residual_range, int tile_cfg, smpq_stream_t stream);
 
+/* ABI 7: a Bottleneck's conv3 (+ limb-plane identity, ReLU) chained with the NEXT block's conv1
+ * (ReLU) in one launch (resnet.py:111-113, then :99-101 of the next block): the second conv reads
+ * the first one's output tile from LDS instead of HBM. Both outputs and the overflow flag are
+ * bitwise those of two smpq_conv2d_fwd_q calls. 3 activation limbs, exact weight codes (no offsets):
+ *   xq, x_absmax, n, h, w, cin          conv3's input, as smpq_conv2d_fwd_q (1x1, stride 1, pad 0)
+ *   codes1 [cout1][cin], col_scale1, col_shift1 [cout1]        conv3 (+ its folded BN)
+ *   residual_q [3][n*h*w][cout1], residual_range               the identity's limb planes
+ *   yq1 [3][n*h*w][cout1], yq1_range    conv3's output limb planes (the next block's identity)
+ *   y1_absmax [n]                       per-image range conv1 reads them with (what a separate
+ *                                       conv1 launch gets as x_absmax)
+ *   codes2 [cout2][cout1], col_scale2, col_shift2 [cout2]      the next block's conv1
+ *   yq2 [3][n*h*w][cout2], yq2_range    conv1's output limb planes
+ *   overflow                            int32 [1]: set when either output exceeded its range
+ * Built for (cin, cout1, cout2) = (64, 256, 64) and (128, 512, 128), the ResNet-50 layer1 / layer2
+ * blocks (smpq_conv2d_pair_supported); other calls return SMPQ_E_INVALID. */
+int smpq_conv2d_pair_supported(int cin, int cout1, int cout2, int limbs);
+int smpq_conv2d_pair_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+                         const int8_t* codes1, int cout1, const float* col_scale1, const float* col_shift1,
+                         const int8_t* residual_q, float residual_range, int8_t* yq1, float yq1_range,
+                         const float* y1_absmax, const int8_t* codes2, int cout2, const float* col_scale2,
+                         const float* col_shift2, int8_t* yq2, float yq2_range, int32_t* overflow,
+                         smpq_stream_t stream);
+
 /* codes [wlimbs][cout][K] (K % 64 == 0, 16-B aligned) -> out [wlimbs][K/64][cout][64], the K-major
  * copy smpq_conv2d_fwd_q_km reads. */
 int smpq_weights_kmajor(const int8_t* codes, int wlimbs, int cout, int K, int8_t* out, smpq_stream_t stream);
@@ -276,13 +299,15 @@ int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads);
  *                              return SMPQ_E_INVALID.
  *                              Its configurations follow the LDS-DMA ones; BM = the tile's pixels
  *                              (TH x TW of one image), BN = 64.
- *   SMPQ_TILE_RESIDENT1X1      (ABI 6) weight-stationary 1x1 tiles: 1x1 / pad 0 convs with cin 64,
- *                              cout 256, 3 activation limbs, 1 or 3 weight limbs, no weight offsets,
- *                              static-range limb-plane output without a residual (yq set; y,
- *                              y_absmax, residual, residual_q NULL; relu either) — other calls return
- *                              SMPQ_E_INVALID. A persistent workgroup keeps every weight limb in
- *                              registers and walks pixel tiles; BM = pixels per tile, BN = 256.
- *                              Its configurations follow the halo ones.
+ *   SMPQ_TILE_RESIDENT1X1      (ABI 6) weight-stationary 1x1 tiles: 1x1 / pad 0 convs with cin
+ *                              64 .. 1024 (per configuration: smpq_conv2d_tile_supported), cout a
+ *                              multiple of the slab (BN = 64 / 128 / 256), 3 activation limbs, no
+ *                              weight offsets, static-range limb-plane output (yq set; y, y_absmax,
+ *                              residual NULL); 3 weight limbs without ReLU or residual_q (the
+ *                              downsamples), 1 weight limb with ReLU and optionally residual_q, or
+ *                              neither — other calls return SMPQ_E_INVALID. A persistent workgroup
+ *                              keeps its slab's weight limbs in registers and walks pixel tiles;
+ *                              BM = pixels per tile, BN = the slab. Configurations follow the halo ones.
  * (negative: error code). Values 0 and 1 were the register-staged family (ABI <= 3, removed). */
 #define SMPQ_TILE_LDS_DMA 2
 #define SMPQ_TILE_LDS_DMA_K128 3

@@ -632,3 +632,29 @@ extern "C" int smpq_debug_mfma_i8(const int8_t* a, const int8_t* b, int32_t* c, 
   hipLaunchKernelGGL(debug_mfma_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, c);
   return check_hip(hipGetLastError(), "debug_mfma_kernel launch");
 }
+
+extern "C" int smpq_conv2d_pair_supported(int cin, int cout1, int cout2, int limbs) {
+  return resident_pair_supported(cin, cout1, cout2, limbs) ? 1 : 0;
+}
+
+extern "C" int smpq_conv2d_pair_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+                                    const int8_t* codes1, int cout1, const float* col_scale1,
+                                    const float* col_shift1, const int8_t* residual_q, float residual_range,
+                                    int8_t* yq1, float yq1_range, const float* y1_absmax, const int8_t* codes2,
+                                    int cout2, const float* col_scale2, const float* col_shift2, int8_t* yq2,
+                                    float yq2_range, int32_t* overflow, smpq_stream_t stream) {
+  constexpr int limbs = 3;
+  if (!yq1 || !yq2 || !residual_q || !y1_absmax)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_pair_fwd: null pointer");
+  ConvArgs a, b;
+  int rc = conv_args_q(xq, x_absmax, n, h, w, cin, codes1, 1, nullptr, cout1, 1, 1, 1, 0, col_scale1, col_shift1,
+                       nullptr, 1, limbs, nullptr, nullptr, yq1, yq1_range, overflow, residual_q, residual_range, a);
+  if (rc) return rc;
+  // the second conv reads the first one's output planes: as a separate launch, on yq1 with y1_absmax
+  rc = conv_args_q(yq1, y1_absmax, n, h, w, cout1, codes2, 1, nullptr, cout2, 1, 1, 1, 0, col_scale2, col_shift2,
+                   nullptr, 1, limbs, nullptr, nullptr, yq2, yq2_range, overflow, nullptr, 0.f, b);
+  if (rc) return rc;
+  const long long big = (long long)limbs * a.M * (cout1 > cin ? cout1 : cin);
+  if (big > 0x7fffff00LL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_pair_fwd: a limb plane of 2 GiB or more");
+  return launch_resident_pair(a, b, limbs, (hipStream_t)stream);
+}

@@ -22,6 +22,15 @@
 // ahead, as a [L][BP][BN] tile in the output tile's layout. The slabs of a conv
 // walk the same pixel tiles in the same order, so a tile's activations are read from HBM once and
 // from L2 / MALL by the other slabs.
+//
+// Chained pair (CW2 > 0; smpq_conv2d_pair_fwd, round 6): a Bottleneck's conv3 (+ limb-plane identity,
+// ReLU) followed by the NEXT block's conv1 (1x1, ReLU), which reads nothing but conv3's output
+// (resnet.py:108-113 then :99-101). One slab holds all of conv3's channels, so the staged output tile
+// [L][BP][BN] is exactly conv1's activation tile for the same pixels: after it is written, its limb
+// rows are read straight back as conv1's MFMA B fragments (conv1's weights: a second set of VGPR
+// fragments), and conv1's own [L][BP][64 CW2] tile is staged and copied out beside it. Both outputs
+// are bitwise those of the two separate launches (the same codes, the same epilogue); conv1's
+// activation read from HBM disappears.
 #include "conv_common.h"
 #include "lds_dma.h"
 
@@ -55,24 +64,28 @@ __device__ __forceinline__ int ach(int c, int r) {
   else return c ^ (r & 15);
 }
 
-template <int L, int LW, int KC, int CW, int WP, bool RES>
+template <int L, int LW, int KC, int CW, int WP, bool RES, int CW2 = 0>
 struct ResShape {
   static constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
   static constexpr int NACC = L + LW - 1 - SMIN;
   static constexpr int BN = 64 * CW, BP = 16 * WP, K = 64 * KC;
   static constexpr int ASTAGE = L * BP * K;  // activation tile bytes
   static constexpr int OTILE = L * BP * BN;  // output (and residual) tile bytes
-  static constexpr int LDS = 2 * ASTAGE + (RES ? 3 : 1) * OTILE;
-  // VGPRs: weights + accumulators + one chunk's B fragments + addressing / epilogue (~40)
-  static constexpr int REGS = 4 * (LW * KC * CW + NACC * CW * WP + L * WP) + 40;
-  static constexpr int MINW_R = REGS <= 128 ? 4 : (REGS <= 160 ? 3 : 2);  // workgroups per CU (1 wave per SIMD each)
+  static constexpr int OTILE2 = L * BP * 64 * CW2;  // the chained conv's output tile
+  static constexpr int LDS = 2 * ASTAGE + (RES ? 3 : 1) * OTILE + OTILE2;
+  // VGPRs: weights (+ the chained conv's) + accumulators + one chunk's B fragments + addressing /
+  // epilogue (~40)
+  static constexpr int REGS = 4 * (LW * KC * CW + CW * CW2 + NACC * CW * WP + L * WP) + 40;
+  // workgroups per CU (1 wave per SIMD each; past 256 the accumulators move to AGPRs)
+  static constexpr int MINW_R = REGS <= 128 ? 4 : (REGS <= 160 ? 3 : (REGS <= 240 ? 2 : 1));
   static constexpr int MINW_L = (160 * 1024) / LDS;
   static constexpr int MINW = MINW_R < MINW_L ? MINW_R : MINW_L;
 };
 
-template <int L, int LW, int KC, int CW, int WP, bool RELU, bool RES, int MINW>
-__global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvArgs a, int ntiles, int nslabs) {
-  using S = ResShape<L, LW, KC, CW, WP, RES>;
+template <int L, int LW, int KC, int CW, int WP, bool RELU, bool RES, int MINW, int CW2 = 0>
+__global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvArgs a, ConvArgs b, int ntiles,
+                                                                           int nslabs) {
+  using S = ResShape<L, LW, KC, CW, WP, RES, CW2>;
   constexpr int SMIN = S::SMIN, NACC = S::NACC, BN = S::BN, BP = S::BP, K = S::K, ASTAGE = S::ASTAGE;
   constexpr int CH = K / 16;       // 16-B chunks per activation row
   constexpr int RP = 1024 / K;     // activation rows per 1-KiB DMA piece
@@ -106,6 +119,21 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
         const v4u v = __builtin_amdgcn_raw_buffer_load_b128(wrs, off, (unsigned)(lw * a.wplane), 0);
         wa[lw][kc][i] = v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
       }
+  // the chained conv's weights (CW2 > 0: exact codes, K = BN = this conv's output channels, KC2 = CW
+  // chunks of 64; wave w: its output channels 16 (CW2 w + i) + p)
+  constexpr int KC2 = CW2 > 0 ? CW : 0, BN2 = 64 * CW2;
+  v4i wb[KC2 > 0 ? KC2 : 1][CW2 > 0 ? CW2 : 1];
+  if constexpr (CW2 > 0) {
+    const auto wrs2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(b.codes), 0, (int)b.wplane, 0x00020000);
+#pragma unroll
+    for (int kc = 0; kc < KC2; ++kc)
+#pragma unroll
+      for (int i = 0; i < CW2; ++i) {
+        const int row = (wave * CW2 + i) * 16 + frow;
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(wrs2, (unsigned)(row * BN + kc * 64 + 16 * grp), 0u, 0);
+        wb[kc][i] = v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+      }
+  }
 
   // ---- activation DMA: piece = RP pixel rows x K bytes of one limb; lane -> (row, physical chunk)
   const int prow = lane / CH, pphys = lane % CH;
@@ -162,17 +190,70 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
   const float lo = RELU ? 0.f : -qmax;
   const float rsq = a.res_scale * inv;
   const v4i qrs4 = make_rsrc(a.yq, (long long)L * oplane);
+  // the chained conv's epilogue constants, output planes and staged tile
+  const float inv2 = CW2 > 0 ? b.yq_inv : 0.f;
+  float csq2[CW2 > 0 ? CW2 : 1][4], shq2[CW2 > 0 ? CW2 : 1][4];
+  if constexpr (CW2 > 0) {
+#pragma unroll
+    for (int i = 0; i < CW2; ++i) {
+      const int c = (wave * CW2 + i) * 16 + 4 * grp;
+      const float4 cs = *reinterpret_cast<const float4*>(b.col_scale + c);
+      const float4 csh = *reinterpret_cast<const float4*>(b.col_shift + c);
+      csq2[i][0] = cs.x * inv2, csq2[i][1] = cs.y * inv2, csq2[i][2] = cs.z * inv2, csq2[i][3] = cs.w * inv2;
+      shq2[i][0] = csh.x * inv2, shq2[i][1] = csh.y * inv2, shq2[i][2] = csh.z * inv2, shq2[i][3] = csh.w * inv2;
+    }
+  }
+  const long long oplane2 = CW2 > 0 ? (long long)a.M * BN2 : 0;
+  const v4i qrs4b = make_rsrc(CW2 > 0 ? b.yq : nullptr, (long long)L * oplane2);
+  int8_t* const otile2 = lds + 2 * ASTAGE + (RES ? 3 : 1) * OTILE;
   const bool nt = __builtin_amdgcn_readfirstlane(a.nt_store) != 0;
   float vmax = 0.f;
 
-  int stage = 0;
+  // copy-out of a staged output tile: BN-byte pixel rows of the slab, 16 B per lane
+  auto copy_out = [&](int m0) {
+    constexpr int RC = BN / 16, ITEMS = L * BP * RC;
+#pragma unroll
+    for (int k = 0; k < (ITEMS + kResThreads - 1) / kResThreads; ++k) {
+      const int it = threadIdx.x + kResThreads * k;
+      if (ITEMS % kResThreads == 0 || it < ITEMS) {
+        const int l = it / (BP * RC), rem = it - l * (BP * RC);
+        const int rt = rem / RC, c = rem - rt * RC;
+        const v4i v = *reinterpret_cast<const v4i*>(otile + l * BP * BN + rt * BN + 16 * (c ^ swze<BN>(rt & 15)));
+        const unsigned off = m0 + rt < a.M ? (unsigned)((long long)(m0 + rt) * a.cout + n0 + 16 * c) : kOOB;
+        store_limbs16(v4u{(unsigned)v.x, (unsigned)v.y, (unsigned)v.z, (unsigned)v.w}, qrs4, off,
+                      __builtin_amdgcn_readfirstlane((unsigned)((long long)l * oplane)), nt);
+      }
+    }
+    if constexpr (CW2 > 0) {
+      constexpr int RC2 = BN2 / 16, ITEMS2 = L * BP * RC2;
+#pragma unroll
+      for (int k = 0; k < (ITEMS2 + kResThreads - 1) / kResThreads; ++k) {
+        const int it = threadIdx.x + kResThreads * k;
+        if (ITEMS2 % kResThreads == 0 || it < ITEMS2) {
+          const int l = it / (BP * RC2), rem = it - l * (BP * RC2);
+          const int rt = rem / RC2, c = rem - rt * RC2;
+          const v4i v = *reinterpret_cast<const v4i*>(otile2 + l * BP * BN2 + rt * BN2 + 16 * (c ^ swze<BN2>(rt & 15)));
+          const unsigned off = m0 + rt < a.M ? (unsigned)((long long)(m0 + rt) * BN2 + 16 * c) : kOOB;
+          store_limbs16(v4u{(unsigned)v.x, (unsigned)v.y, (unsigned)v.z, (unsigned)v.w}, qrs4b, off,
+                        __builtin_amdgcn_readfirstlane((unsigned)((long long)l * oplane2)), nt);
+        }
+      }
+    }
+  };
+  // Tile loop. The copy-out of tile i-1 and the DMA of tile i+1 are issued at the top of
+  // iteration i, before tile i's MFMAs and epilogue, so both fly under a tile's work; raw s_barriers
+  // with explicit waits (a __syncthreads would also wait for the stores and the DMA).
+  int stage = 0, prev_m0 = -1;
   for (; t < ntiles; t += tstride) {
     const int m0 = t * BP;
-    // tile t's activations have landed (this wave's pieces; after the barrier every wave's), and
-    // every wave is past the previous tile's copy-out and its reads of the other stage
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t + tstride < ntiles) {  // under this tile's work
+    // tile t's activations (and residual) have landed and the last copy-out's stores are done (this
+    // wave's); every wave's epilogue writes of the staged output tile and its reads of the other
+    // stage are done (lgkmcnt) — after the barrier, every wave's
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (prev_m0 >= 0) copy_out(prev_m0);
+    if (t + tstride < ntiles) {
       issue_acts(t + tstride, stage ^ 1);
       issue_res(t + tstride, stage ^ 1);
     }
@@ -207,6 +288,10 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
                   __builtin_amdgcn_mfma_i32_16x16x64_i8(wa[lw][kc][i], fb[l][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
         }
     }
+    // every wave's copy-out reads of the staged output tile are done before it is overwritten
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     // lean epilogue -> the [L][BP][BN] output tile in LDS (16-B chunk c of tile row r at
     // c ^ swze<BN>(r & 15), as the LDS-DMA kernel's staged tiles)
 #pragma unroll
@@ -236,22 +321,65 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
           *reinterpret_cast<unsigned*>(otile + l * BP * BN + rt * BN + 16 * (cc ^ swze<BN>(frow)) + 4 * grp) = wq[l];
       }
     }
-    __syncthreads();
-    // copy-out: BN-byte pixel rows of the slab, 16 B per lane
-    constexpr int RC = BN / 16, ITEMS = L * BP * RC;
+    if constexpr (CW2 > 0) {
+      // the chained conv on the staged tile: every wave's epilogue writes are done (barrier), then
+      // its limb rows are the B fragments (row r, K chunk 4 kc + g at (4 kc + g) ^ swze<BN>(r & 15))
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      v4i acc2[L][CW2][WP];
 #pragma unroll
-    for (int k = 0; k < (ITEMS + kResThreads - 1) / kResThreads; ++k) {
-      const int it = threadIdx.x + kResThreads * k;
-      if (ITEMS % kResThreads == 0 || it < ITEMS) {
-        const int l = it / (BP * RC), rem = it - l * (BP * RC);
-        const int rt = rem / RC, c = rem - rt * RC;
-        const v4i v = *reinterpret_cast<const v4i*>(otile + l * BP * BN + rt * BN + 16 * (c ^ swze<BN>(rt & 15)));
-        const unsigned off = m0 + rt < a.M ? (unsigned)((long long)(m0 + rt) * a.cout + n0 + 16 * c) : kOOB;
-        store_limbs16(v4u{(unsigned)v.x, (unsigned)v.y, (unsigned)v.z, (unsigned)v.w}, qrs4, off,
-                      __builtin_amdgcn_readfirstlane((unsigned)((long long)l * oplane)), nt);
+      for (int s = 0; s < L; ++s)
+#pragma unroll
+        for (int i = 0; i < CW2; ++i)
+#pragma unroll
+          for (int j = 0; j < WP; ++j) acc2[s][i][j] = v4i{0, 0, 0, 0};
+#pragma unroll
+      for (int kc = 0; kc < KC2; ++kc) {
+        v4i fb[L][WP];
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+#pragma unroll
+          for (int j = 0; j < WP; ++j) {
+            const int r = j * 16 + frow;
+            fb[l][j] = *reinterpret_cast<const v4i*>(otile + l * BP * BN + r * BN + 16 * ((4 * kc + grp) ^ swze<BN>(frow)));
+          }
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+#pragma unroll
+          for (int i = 0; i < CW2; ++i)
+#pragma unroll
+            for (int j = 0; j < WP; ++j)
+              acc2[l][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wb[kc][i], fb[l][j], acc2[l][i][j], 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < WP; ++j) {
+        const int m = m0 + j * 16 + frow;
+        const float rscale = m < a.M ? b.x_absmax[fast_div(m, a.hw_mul, a.hw_shr)] * b.inv_qmax : 0.f;
+#pragma unroll
+        for (int i = 0; i < CW2; ++i) {
+          v4i accq[L];
+#pragma unroll
+          for (int s = 0; s < L; ++s) accq[s] = acc2[s][i][j];
+          const int rt = j * 16 + frow, cc = wave * CW2 + i;
+          const int rq0[4] = {0, 0, 0, 0};
+          unsigned wq[L];
+          const float mm = lean_quad<L, L, 0>(accq, rscale, csq2[i], shq2[i], false, rq0, 0.f, true, 0.f, wq);
+          vmax = m < a.M ? fmaxf(vmax, mm) : vmax;
+#pragma unroll
+          for (int l = 0; l < L; ++l)
+            *reinterpret_cast<unsigned*>(otile2 + l * BP * BN2 + rt * BN2 + 16 * (cc ^ swze<BN2>(frow)) + 4 * grp) = wq[l];
+        }
       }
     }
+    prev_m0 = m0;
     stage ^= 1;
+  }
+  if (prev_m0 >= 0) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    copy_out(prev_m0);
   }
   if (__any(vmax > qmax) && lane == 0) atomicMax(a.overflow, 1);
 }
@@ -293,7 +421,7 @@ int launch_res_one(const ConvArgs& a, hipStream_t s) {
   if (per_slab < 1) per_slab = 1;
   if (per_slab > ntiles) per_slab = ntiles;
   const long long blocks = per_slab * nslabs;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kResThreads), S::LDS, s, a, (int)ntiles, nslabs);
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kResThreads), S::LDS, s, a, a, (int)ntiles, nslabs);
   return check_hip(hipGetLastError(), "qconv_resident_kernel launch");
   }
 }
@@ -319,6 +447,27 @@ int launch_res_l(int cfg, const ConvArgs& a, hipStream_t s) {
     case 2: return launch_res_kc<L, LW, 2, RELU, RES>(kc, a, s);
     default: return launch_res_kc<L, LW, 3, RELU, RES>(kc, a, s);
   }
+}
+
+// the chained pair (CW2 > 0): one slab with all of the first conv's output channels, 16-pixel tiles
+template <int L, int KC, int CW, int CW2>
+int launch_pair_one(const ConvArgs& a, const ConvArgs& b, hipStream_t s) {
+  using S = ResShape<L, 1, KC, CW, 1, true, CW2>;
+  static_assert(S::MINW >= 1, "LDS per CU");
+  auto k = qconv_resident_kernel<L, 1, KC, CW, 1, true, true, S::MINW, CW2>;
+  static const hipError_t attr = [&] {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
+    if (e != hipSuccess) (void)hipGetLastError();
+    return e;
+  }();
+  if (attr != hipSuccess) return check_hip(attr, "qconv_resident_kernel (pair) LDS attribute");
+  const long long ntiles = ((long long)a.M + S::BP - 1) / S::BP;
+  long long blocks = (long long)device_cus_res() * S::MINW;
+  if (blocks > ntiles) blocks = ntiles;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kResThreads), S::LDS, s, a, b, (int)ntiles, 1);
+  return check_hip(hipGetLastError(), "qconv_resident_kernel (pair) launch");
 }
 
 }  // namespace
@@ -359,6 +508,25 @@ int launch_resident(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream
     return launch_res_l<3, 1, true, true>(cfg, a, s);
   }
   return a.relu ? launch_res_l<3, 1, true, false>(cfg, a, s) : launch_res_l<3, 1, false, false>(cfg, a, s);
+}
+
+// Bottleneck conv3 (+ limb-plane identity, ReLU) chained with the next block's conv1 (ReLU):
+// (cin, cout1, cout2) = (64, 256, 64) (the R50 layer1 blocks) or (128, 512, 128) (layer2)
+bool resident_pair_supported(int cin, int cout1, int cout2, int limbs) {
+  return limbs == 3 && ((cin == 64 && cout1 == 256 && cout2 == 64) || (cin == 128 && cout1 == 512 && cout2 == 128));
+}
+
+int launch_resident_pair(const ConvArgs& a, const ConvArgs& b, int limbs, hipStream_t s) {
+  if (!resident_pair_supported(a.cin, a.cout, b.cout, limbs) || a.kh != 1 || a.kw != 1 || a.stride != 1 ||
+      a.pad != 0 || b.kh != 1 || b.kw != 1 || b.stride != 1 || b.pad != 0 || b.cin != a.cout || b.M != a.M)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_pair_fwd: shapes not built (64->256->64 or 128->512->128 1x1, "
+                                "stride 1, 3 activation limbs, the second conv on the first one's output)");
+  if (!a.yq || !b.yq || a.y || b.y || a.residual || !a.res_q || b.res_q || b.residual || a.y_absmax ||
+      b.y_absmax || a.has_offset || b.has_offset || !a.relu || !b.relu || a.overflow != b.overflow)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_pair_fwd: static-range limb-plane outputs, ReLU, a limb-plane "
+                                "residual on the first conv only, exact weight codes, one overflow flag");
+  if (a.cin == 64) return launch_pair_one<3, 1, 4, 1>(a, b, s);
+  return launch_pair_one<3, 2, 8, 2>(a, b, s);
 }
 
 }  // namespace smpq

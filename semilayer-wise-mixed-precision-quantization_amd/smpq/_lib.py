@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must be imported before the library; see module doc
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsmpq.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lib = None
 _lock = threading.Lock()
@@ -54,6 +54,9 @@ _PROTOS = {
     "smpq_conv2d_fwd_q_km": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp,
                                   _vp, _i, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, ctypes.c_float, _i, _vp]),
     "smpq_weights_kmajor": (_i, [_vp, _i, _i, _i, _vp, _vp]),
+    "smpq_conv2d_pair_supported": (_i, [_i] * 4),
+    "smpq_conv2d_pair_fwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, ctypes.c_float, _vp,
+                                  ctypes.c_float, _vp, _vp, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _vp]),
     "smpq_maxpool_limbs": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "smpq_image_quantize_s2d": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
     "smpq_pack_weights_s2d": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _vp]),

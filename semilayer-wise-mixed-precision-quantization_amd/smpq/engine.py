@@ -70,6 +70,11 @@ FUSED_STEM = [_os.environ.get("SMPQ_FUSED_STEM", "1") != "0"]
 CONCURRENT_DS = [_os.environ.get("SMPQ_CONCURRENT_DS", "1") != "0"]
 # static range: the batch split into this many slices, each on its own stream (concurrent kernels)
 STREAMS = [int(_os.environ.get("SMPQ_STREAMS", "2"))]
+# static range: a Bottleneck's conv3 and the next block's conv1 as ONE launch where the pair kernel
+# is built (ops.conv_pair_q: conv1 reads conv3's output tile from LDS; bitwise the two launches)
+PAIR_1X1 = [_os.environ.get("SMPQ_PAIR_1X1", "1") != "0"]
+# ... for the chains whose conv3 has at most this many input channels (64: layer1 only)
+PAIR_MAX_CIN = [int(_os.environ.get("SMPQ_PAIR_MAX_CIN", "128"))]
 stats.setdefault("graph_captures", 0)
 stats.setdefault("graph_replays", 0)
 
@@ -254,8 +259,37 @@ def _side_stream(device, lane):
     return _stream((device, "ds", lane))
 
 
-def block_forward(blk, x, ctx=None, last=False):
-    """One BasicBlock / Bottleneck on an Act; returns the output Act. In static mode no
+def _pair_plan(blk, nxt, ctx, identity):
+    """(conv3 plan, next conv1 plan) when blk.conv3 and nxt.conv1 can run as one pair launch
+    (static ranges, exact codes, 1x1 / stride 1 / pad 0 both, a limb-plane identity, a built
+    shape), else None."""
+    if not (PAIR_1X1[0] and nxt is not None and ctx is not None and ctx.ranges is not None
+            and hasattr(blk, "conv3") and hasattr(nxt, "conv3") and nxt.downsample is None
+            and isinstance(identity, Act) and identity.f32 is None and identity.q is not None
+            and identity.rng is not None):
+        return None
+    c3, c1 = blk.conv3, nxt.conv1
+    if c3.in_channels > PAIR_MAX_CIN[0] or id(c3) not in ctx.ranges or id(c1) not in ctx.ranges:
+        return None
+    for c in (c3, c1):
+        if c.kernel_size != (1, 1) or c.stride != (1, 1) or c.padding != (0, 0) or c.groups != 1:
+            return None
+    p3, p1 = conv_plan(c3, blk.bn3), conv_plan(c1, nxt.bn1)
+    if p3 is None or p1 is None:
+        return None
+    for codes, offset in ((p3[0], p3[1]), (p1[0], p1[1])):
+        if offset is not None or not (codes.dim() == 2 or codes.shape[0] == 1):
+            return None
+    if identity.q.shape[0] != 3 or not ops.conv_pair_supported(c3.in_channels, c3.out_channels, c1.out_channels):
+        return None
+    return p3, p1
+
+
+def block_forward(blk, x, ctx=None, last=False, t1=None, nxt=None):
+    """One BasicBlock / Bottleneck on an Act; returns (output Act, the next block's conv1 output
+    Act or None). ``t1``: this block's conv1 output when the previous block already computed it
+    (pair launch); ``nxt``: the next block, whose conv1 is chained onto this block's conv3 when
+    _pair_plan allows. In static mode no
     activation is stored in fp32 except the downsample's identity and the last block's output
     (avgpool): the identity of a block without downsample is read from its input's limb planes.
 
@@ -292,16 +326,30 @@ def block_forward(blk, x, ctx=None, last=False):
         if side is not None:
             torch.cuda.current_stream().wait_stream(side)
 
-    t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
+    if t1 is None:
+        t1 = run_conv(blk.conv1, blk.bn1, x, True, ctx=ctx, want_f32=False)
     if hasattr(blk, "conv3"):  # Bottleneck (resnet.py:97-116)
         t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
         join()
+        pair = None if last else _pair_plan(blk, nxt, ctx, identity)
+        if pair is not None and t2.q is not None and t2.amax is not None:
+            # conv3 (+ identity, ReLU) and the next block's conv1 (ReLU) in one launch
+            (codes3, _, cs3, sh3, kind3), (codes1, _, cs1, sh1, kind1) = pair
+            c3, c1 = blk.conv3, nxt.conv1
+            rng3, rng1 = ctx.ranges[id(c3)], ctx.ranges[id(c1)]
+            am3 = ctx.range_tensor(c3)
+            yq3, yq1 = ops.conv_pair_q(t2.q, t2.amax, codes3, cs3, sh3, identity.q, identity.rng, rng3, am3,
+                                       codes1, cs1, sh1, rng1, ctx.overflow)
+            stats["hip_conv"] += 2
+            stats["pair_conv"] = stats.get("pair_conv", 0) + 1
+            c3.last_path, c1.last_path = "hip-%s-pair" % kind3, "hip-%s-pair" % kind1
+            return Act(q=yq3, amax=am3, rng=rng3), Act(q=yq1, amax=ctx.range_tensor(c1), rng=rng1)
         return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax,
-                        want_f32=last)
+                        want_f32=last), None
     # BasicBlock (resnet.py:55-68)
     join()
     return run_conv(blk.conv2, blk.bn2, t1, True, residual=identity, ctx=ctx, want_amax=out_amax,
-                    want_f32=last)
+                    want_f32=last), None
 
 
 def stem_s2d_plan(conv, bn):
@@ -401,8 +449,10 @@ def _head(model, feat, out=None):
 def _features(model, x, ctx):
     act = stem_forward(model, x, ctx)
     blocks = _blocks(model)
+    t1 = None
     for i, blk in enumerate(blocks):
-        act = block_forward(blk, act, ctx, last=(i == len(blocks) - 1))
+        nxt = blocks[i + 1] if i + 1 < len(blocks) else None
+        act, t1 = block_forward(blk, act, ctx, last=nxt is None, t1=t1, nxt=nxt)
     return act.f32
 
 
@@ -618,7 +668,7 @@ def _graph_base(cal):
     """What every captured graph of a model depends on besides its input's shape and address:
     the calibration (ranges, signature) and the forward's structure knobs."""
     return (cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0], CONCURRENT_DS[0], STREAMS[0],
-            ops.KMAJOR[0])
+            ops.KMAJOR[0], PAIR_1X1[0], PAIR_MAX_CIN[0])
 
 
 def _graph_key(model, x, cal):

@@ -500,6 +500,76 @@ def conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, col_sh
 PLANE_LIMIT = 0x7fffff00
 
 
+def conv_pair_supported(cin, cout1, cout2, limbs=3):
+    """Does smpq_conv2d_pair_fwd run this Bottleneck chain (conv3 cin -> cout1, next conv1 cout1 ->
+    cout2)?"""
+    return bool(_lib.load().smpq_conv2d_pair_supported(int(cin), int(cout1), int(cout2), int(limbs)))
+
+
+def conv_pair_q(xq, x_absmax, codes1, col_scale1, col_shift1, residual_q, residual_range, emit_range1,
+                y1_absmax, codes2, col_scale2, col_shift2, emit_range2, overflow):
+    """A Bottleneck's conv3 (1x1 + folded BN + limb-plane identity + ReLU) chained with the next
+    block's conv1 (1x1 + folded BN + ReLU) in one launch (csrc/conv_resident.hip, the pair path):
+    returns (yq1, yq2), bitwise
+
+        _, yq1 = conv2d_q(xq, x_absmax, codes1, None, 1, 1, 1, 0, col_scale1, col_shift1, relu=True,
+                          emit_range=emit_range1, overflow=overflow, want_f32=False,
+                          residual_q=residual_q, residual_range=residual_range)
+        _, yq2 = conv2d_q(yq1, y1_absmax, codes2, None, 1, 1, 1, 0, col_scale2, col_shift2, relu=True,
+                          emit_range=emit_range2, overflow=overflow, want_f32=False)
+
+    without reading yq1 back from HBM. Exact weight codes only (one limb, no offsets)."""
+    _req(xq.is_cuda and xq.dtype == torch.int8 and xq.dim() == 5 and xq.is_contiguous(), "pair: xq")
+    limbs, n, h, w, cin = xq.shape
+    c1 = codes1[0] if codes1.dim() == 3 else codes1
+    c2 = codes2[0] if codes2.dim() == 3 else codes2
+    _req(codes1.dim() == 2 or codes1.shape[0] == 1, "pair: conv3 needs exact codes (one weight limb)")
+    _req(codes2.dim() == 2 or codes2.shape[0] == 1, "pair: conv1 needs exact codes (one weight limb)")
+    cout1, cout2 = c1.shape[0], c2.shape[0]
+    _req(c1.shape == (cout1, cin) and c2.shape == (cout2, cout1) and c1.is_contiguous() and c2.is_contiguous()
+         and c1.dtype == torch.int8 and c2.dtype == torch.int8, "pair: codes shapes")
+    _req(conv_pair_supported(cin, cout1, cout2, limbs), "pair: shape not built")
+    _req(residual_q.shape == (limbs, n, h, w, cout1) and residual_q.dtype == torch.int8
+         and residual_q.is_contiguous(), "pair: residual_q")
+    _req(x_absmax.numel() == n and y1_absmax.numel() == n, "pair: absmax")
+    for t, c in ((col_scale1, cout1), (col_shift1, cout1), (col_scale2, cout2), (col_shift2, cout2)):
+        _req(t.dtype == torch.float32 and t.numel() == c and t.is_contiguous() and t.device == xq.device,
+             "pair: col vectors")
+    _req(overflow is not None and overflow.dtype == torch.int32 and overflow.device == xq.device, "pair: overflow")
+    nchunk = PLANE_LIMIT // (limbs * h * w * max(cin, cout1))
+    _req(nchunk >= 1, "pair: one image's planes exceed 2 GiB")
+    if n > nchunk:  # 32-bit buffer offsets: image chunks (independent images, the same result)
+        yq1 = torch.empty(limbs, n, h, w, cout1, dtype=torch.int8, device=xq.device)
+        yq2 = torch.empty(limbs, n, h, w, cout2, dtype=torch.int8, device=xq.device)
+        for i0 in range(0, n, nchunk):
+            i1 = min(n, i0 + nchunk)
+            a, b = conv_pair_q(xq[:, i0:i1].contiguous(), x_absmax[i0:i1], codes1, col_scale1, col_shift1,
+                               residual_q[:, i0:i1].contiguous(), residual_range, emit_range1, y1_absmax[i0:i1],
+                               codes2, col_scale2, col_shift2, emit_range2, overflow)
+            yq1[:, i0:i1].copy_(a)
+            yq2[:, i0:i1].copy_(b)
+        return yq1, yq2
+    yq1 = torch.empty(limbs, n, h, w, cout1, dtype=torch.int8, device=xq.device)
+    yq2 = torch.empty(limbs, n, h, w, cout2, dtype=torch.int8, device=xq.device)
+    lib = _lib.load()
+    hook = _CONV_HOOK[0]
+    if hook is not None:
+        hook.begin()
+    with torch.cuda.device(xq.device):
+        _lib.check(lib.smpq_conv2d_pair_fwd(
+            _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, cin, _lib.ptr(c1), cout1, _lib.ptr(col_scale1),
+            _lib.ptr(col_shift1), _lib.ptr(residual_q), float(residual_range), _lib.ptr(yq1), float(emit_range1),
+            _lib.ptr(y1_absmax), _lib.ptr(c2), cout2, _lib.ptr(col_scale2), _lib.ptr(col_shift2), _lib.ptr(yq2),
+            float(emit_range2), _lib.ptr(overflow), _lib.stream_ptr()), "smpq_conv2d_pair_fwd")
+    if hook is not None:
+        # one launch doing both convs' work; the second conv's activation read is gone
+        w1 = alg_work(n, h, w, cin, cout1, 1, 1, h, w, limbs, 1, False, True, False, True)
+        w2 = alg_work(n, h, w, cout1, cout2, 1, 1, h, w, limbs, 1, False, True, False, False)
+        hook.end({"ops": w1["ops"] + w2["ops"], "bytes": w1["bytes"] + w2["bytes"] - limbs * n * h * w * cout1,
+                  "passes": w1["passes"], "shape": "%4d->%4d->%4d k1 %3d pair" % (cin, cout1, cout2, h)})
+    return yq1, yq2
+
+
 # ---- per-shape tile choice (cf. cudnn.benchmark=True, resnet50_main.py:10) ---------------------
 # Every tile configuration gives bitwise-identical results; only the time differs. A shape's tile
 # comes from (1) this process's cache, (2) the committed table smpq/data/tiles_gfx950.json

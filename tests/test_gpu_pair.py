@@ -1,0 +1,130 @@
+"""The chained Bottleneck pair (csrc/conv_resident.hip, smpq_conv2d_pair_fwd): a block's conv3
+(+ limb-plane identity, ReLU) and the next block's conv1 (ReLU) in one launch give both outputs'
+limb planes and the overflow flag bit for bit as the two separate launches — in range and with
+either output overflowing, partial last tiles, many tiles per workgroup — and the R50 forward with
+the pair launches on equals the forward without them (eager and graph-replayed). Every call goes
+through the C-ABI."""
+import pytest
+import torch
+
+from test_gpu import build_model, make_layer
+
+pytestmark = pytest.mark.gpu
+
+
+def _chain(gpu, cin, cout1, cout2, n, h, seed):
+    from smpq import ops
+    _, _, codes1, _ = make_layer(gpu, cin, cout1, 1, seed=seed, bits_choice=(8, 6, 4))
+    _, _, codes2, _ = make_layer(gpu, cout1, cout2, 1, seed=seed + 1, bits_choice=(6, 4))
+    g = torch.Generator().manual_seed(seed + 2)
+    x = torch.relu(torch.randn(n, h, h, cin, generator=g)).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, 3)
+    r = torch.relu(torch.randn(n, h, h, cout1, generator=g)).to(gpu)
+    rr = float(r.abs().max()) * 1.25
+    rq = ops.act_quantize(r, torch.full((n,), rr, device=gpu), 3)
+    cs1 = (torch.rand(cout1, generator=g) * 0.02 + 0.01).to(gpu)
+    sh1 = torch.linspace(-0.3, 0.3, cout1).to(gpu)
+    cs2 = (torch.rand(cout2, generator=g) * 0.02 + 0.01).to(gpu)
+    sh2 = torch.linspace(-0.2, 0.4, cout2).to(gpu)
+    return xq, am, codes1, cs1, sh1, rq, rr, codes2, cs2, sh2
+
+
+def _decode(yq):
+    """The int24 codes of [3, ...] balanced limb planes."""
+    return yq[0].long() + 256 * yq[1].long() + 65536 * yq[2].long()
+
+
+def _two_launches(ops, gpu, xq, am, codes1, cs1, sh1, rq, rr, rng1, codes2, cs2, sh2, rng2):
+    n = xq.shape[1]
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+    _, y1 = ops.conv2d_q(xq, am, codes1, None, 1, 1, 1, 0, cs1, sh1, relu=True, emit_range=rng1, overflow=ovf,
+                         want_f32=False, residual_q=rq, residual_range=rr)
+    am1 = torch.full((n,), rng1, device=gpu)
+    _, y2 = ops.conv2d_q(y1, am1, codes2, None, 1, 1, 1, 0, cs2, sh2, relu=True, emit_range=rng2, overflow=ovf,
+                         want_f32=False)
+    return y1, y2, ovf, am1
+
+
+@pytest.mark.parametrize("cin,cout1,cout2,n,h", [
+    (64, 256, 64, 2, 56), (64, 256, 64, 3, 9), (64, 256, 64, 1, 3),
+    (128, 512, 128, 2, 28), (128, 512, 128, 1, 5)])
+def test_pair_equals_two_launches(gpu, cin, cout1, cout2, n, h):
+    from smpq import ops
+    assert ops.conv_pair_supported(cin, cout1, cout2)
+    xq, am, codes1, cs1, sh1, rq, rr, codes2, cs2, sh2 = _chain(gpu, cin, cout1, cout2, n, h, 3 * h + n)
+    # the outputs' magnitudes, from a run with wide ranges
+    y1w, y2w, ovw, _ = _two_launches(ops, gpu, xq, am, codes1, cs1, sh1, rq, rr, 1e4, codes2, cs2, sh2, 1e4)
+    assert int(ovw.item()) == 0
+    m1 = float(_decode(y1w).abs().max()) * 1e4 / 8323072 + 1e-3
+    m2 = float(_decode(y2w).abs().max()) * 1e4 / 8323072 + 1e-3
+    for f1, f2 in ((2.0, 2.0), (0.5, 2.0), (2.0, 0.5), (1.2, 1.1)):
+        rng1, rng2 = m1 * f1, m2 * f2
+        y1, y2, ovf0, am1 = _two_launches(ops, gpu, xq, am, codes1, cs1, sh1, rq, rr, rng1, codes2, cs2, sh2, rng2)
+        if f1 < 1 or f2 < 1:
+            assert int(ovf0.item()) == 1
+        for _ in range(3):  # repeated launches: no race between tiles
+            ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+            p1, p2 = ops.conv_pair_q(xq, am, codes1, cs1, sh1, rq, rr, rng1, am1, codes2, cs2, sh2, rng2, ovf)
+            assert torch.equal(p1, y1), (f1, f2)
+            assert torch.equal(p2, y2), (f1, f2)
+            assert torch.equal(ovf, ovf0), (f1, f2)
+
+
+def test_pair_many_tiles(gpu):
+    """The R50 layer1 shape at 64 images: every workgroup walks ~75 tiles."""
+    from smpq import ops
+    xq, am, codes1, cs1, sh1, rq, rr, codes2, cs2, sh2 = _chain(gpu, 64, 256, 64, 64, 56, 11)
+    y1, y2, ovf0, am1 = _two_launches(ops, gpu, xq, am, codes1, cs1, sh1, rq, rr, 40.0, codes2, cs2, sh2, 40.0)
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+    p1, p2 = ops.conv_pair_q(xq, am, codes1, cs1, sh1, rq, rr, 40.0, am1, codes2, cs2, sh2, 40.0, ovf)
+    assert torch.equal(p1, y1) and torch.equal(p2, y2) and torch.equal(ovf, ovf0)
+
+
+def test_pair_refuses_what_it_does_not_run(gpu):
+    from smpq import _lib, ops
+    assert not ops.conv_pair_supported(256, 1024, 256) and not ops.conv_pair_supported(64, 256, 128)
+    assert not ops.conv_pair_supported(64, 256, 64, 2)
+    xq, am, codes1, cs1, sh1, rq, rr, codes2, cs2, sh2 = _chain(gpu, 64, 256, 64, 1, 4, 5)
+    lib = _lib.load()
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+    y1 = torch.empty(3, 1, 4, 4, 256, dtype=torch.int8, device=gpu)
+    y2 = torch.empty(3, 1, 4, 4, 64, dtype=torch.int8, device=gpu)
+    # no residual: refused before launching
+    rc = lib.smpq_conv2d_pair_fwd(_lib.ptr(xq), _lib.ptr(am), 1, 4, 4, 64, _lib.ptr(codes1), 256, _lib.ptr(cs1),
+                                  _lib.ptr(sh1), None, 0.0, _lib.ptr(y1), 1.0, _lib.ptr(am), _lib.ptr(codes2), 64,
+                                  _lib.ptr(cs2), _lib.ptr(sh2), _lib.ptr(y2), 1.0, _lib.ptr(ovf), _lib.stream_ptr())
+    assert rc == _lib.SMPQ_E_INVALID
+    with pytest.raises(ValueError, match="pair"):  # a shape that is not built
+        ops.conv_pair_q(xq, am, codes1[:128].contiguous(), cs1[:128].contiguous(), sh1[:128].contiguous(),
+                        rq[..., :128].contiguous(), rr, 1.0, am, codes2[:, :128].contiguous(), cs2, sh2, 1.0, ovf)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_r50_forward_with_pairs_bitwise(gpu, graph):
+    """R50 mixed, static ranges, 2 batch slices: the forward with the pair launches (layer1 and
+    layer2) gives the logits of the forward without them, bit for bit."""
+    from smpq import engine, stats
+    net = build_model(gpu, "resnet50", "r50_mixed")
+    x = torch.randn(6, 3, 224, 224, generator=torch.Generator().manual_seed(31)).to(gpu)
+    old = engine.PAIR_1X1[0], engine.USE_GRAPH[0]
+    try:
+        with torch.no_grad():
+            engine.USE_GRAPH[0] = False
+            engine.PAIR_1X1[0] = False
+            net(x)  # calibrate
+            want = net(x)
+            engine.PAIR_1X1[0] = True
+            engine.USE_GRAPH[0] = graph
+            p0 = stats.get("pair_conv", 0)
+            got = [net(x) for _ in range(3)]
+            if not graph:
+                # 3 forwards x 2 slices x the chains whose convs are all exact codes (layer1: 2,
+                # layer2: 3; a conv with unquantized channels runs in fixed point, unpaired)
+                d = stats.get("pair_conv", 0) - p0
+                assert d % 6 == 0 and d // 6 >= 4, d
+            assert net.layer1[1].conv3.last_path.endswith("-pair")
+    finally:
+        engine.PAIR_1X1[0], engine.USE_GRAPH[0] = old
+    for g in got:
+        assert torch.equal(g, want)

@@ -23,7 +23,7 @@ def test_library_exports_every_header_symbol(built_lib):
     for s in syms:
         assert hasattr(built_lib, s), s
         assert s in _lib.EXPORTED_SYMBOLS, s
-    assert built_lib.smpq_abi_version() == 6
+    assert built_lib.smpq_abi_version() == 7
 
 
 def test_loaded_library_matches_the_sources(built_lib):
