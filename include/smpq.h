@@ -212,8 +212,8 @@ int smpq_conv2d_fwd_q_km(const int8_t* xq, const float* x_absmax, int n, int h, 
  *   codes2 [cout2][cout1], col_scale2, col_shift2 [cout2]      the next block's conv1
  *   yq2 [3][n*h*w][cout2], yq2_range    conv1's output limb planes
  *   overflow                            int32 [1]: set when either output exceeded its range
- * Built for (cin, cout1, cout2) = (64, 256, 64) and (128, 512, 128), the ResNet-50 layer1 / layer2
- * blocks (smpq_conv2d_pair_supported); other calls return SMPQ_E_INVALID. */
+ * Built for (cin, cout1, cout2) = (64, 256, 64), the ResNet-50 layer1 blocks
+ * (smpq_conv2d_pair_supported); other calls return SMPQ_E_INVALID. */
 int smpq_conv2d_pair_supported(int cin, int cout1, int cout2, int limbs);
 int smpq_conv2d_pair_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                          const int8_t* codes1, int cout1, const float* col_scale1, const float* col_shift1,

@@ -511,22 +511,23 @@ int launch_resident(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream
 }
 
 // Bottleneck conv3 (+ limb-plane identity, ReLU) chained with the next block's conv1 (ReLU):
-// (cin, cout1, cout2) = (64, 256, 64) (the R50 layer1 blocks) or (128, 512, 128) (layer2)
+// (cin, cout1, cout2) = (64, 256, 64), the R50 layer1 blocks. (The layer2 chain 128 -> 512 -> 128,
+// one 512-channel slab: 452 registers per lane, one workgroup per CU, measured 0.82-0.85x the two
+// launches and the R50 step 1.2 % slower: profiles/r06_pair_chain.txt; not built.)
 bool resident_pair_supported(int cin, int cout1, int cout2, int limbs) {
-  return limbs == 3 && ((cin == 64 && cout1 == 256 && cout2 == 64) || (cin == 128 && cout1 == 512 && cout2 == 128));
+  return limbs == 3 && cin == 64 && cout1 == 256 && cout2 == 64;
 }
 
 int launch_resident_pair(const ConvArgs& a, const ConvArgs& b, int limbs, hipStream_t s) {
   if (!resident_pair_supported(a.cin, a.cout, b.cout, limbs) || a.kh != 1 || a.kw != 1 || a.stride != 1 ||
       a.pad != 0 || b.kh != 1 || b.kw != 1 || b.stride != 1 || b.pad != 0 || b.cin != a.cout || b.M != a.M)
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_pair_fwd: shapes not built (64->256->64 or 128->512->128 1x1, "
-                                "stride 1, 3 activation limbs, the second conv on the first one's output)");
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_pair_fwd: shapes not built (64->256->64 1x1, stride 1, 3 "
+                                "activation limbs, the second conv on the first one's output)");
   if (!a.yq || !b.yq || a.y || b.y || a.residual || !a.res_q || b.res_q || b.residual || a.y_absmax ||
       b.y_absmax || a.has_offset || b.has_offset || !a.relu || !b.relu || a.overflow != b.overflow)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_pair_fwd: static-range limb-plane outputs, ReLU, a limb-plane "
                                 "residual on the first conv only, exact weight codes, one overflow flag");
-  if (a.cin == 64) return launch_pair_one<3, 1, 4, 1>(a, b, s);
-  return launch_pair_one<3, 2, 8, 2>(a, b, s);
+  return launch_pair_one<3, 1, 4, 1>(a, b, s);
 }
 
 }  // namespace smpq

@@ -73,8 +73,6 @@ STREAMS = [int(_os.environ.get("SMPQ_STREAMS", "2"))]
 # static range: a Bottleneck's conv3 and the next block's conv1 as ONE launch where the pair kernel
 # is built (ops.conv_pair_q: conv1 reads conv3's output tile from LDS; bitwise the two launches)
 PAIR_1X1 = [_os.environ.get("SMPQ_PAIR_1X1", "1") != "0"]
-# ... for the chains whose conv3 has at most this many input channels (64: layer1 only)
-PAIR_MAX_CIN = [int(_os.environ.get("SMPQ_PAIR_MAX_CIN", "128"))]
 stats.setdefault("graph_captures", 0)
 stats.setdefault("graph_replays", 0)
 
@@ -269,7 +267,7 @@ def _pair_plan(blk, nxt, ctx, identity):
             and identity.rng is not None):
         return None
     c3, c1 = blk.conv3, nxt.conv1
-    if c3.in_channels > PAIR_MAX_CIN[0] or id(c3) not in ctx.ranges or id(c1) not in ctx.ranges:
+    if id(c3) not in ctx.ranges or id(c1) not in ctx.ranges:
         return None
     for c in (c3, c1):
         if c.kernel_size != (1, 1) or c.stride != (1, 1) or c.padding != (0, 0) or c.groups != 1:
@@ -668,7 +666,7 @@ def _graph_base(cal):
     """What every captured graph of a model depends on besides its input's shape and address:
     the calibration (ranges, signature) and the forward's structure knobs."""
     return (cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0], CONCURRENT_DS[0], STREAMS[0],
-            ops.KMAJOR[0], PAIR_1X1[0], PAIR_MAX_CIN[0])
+            ops.KMAJOR[0], PAIR_1X1[0])
 
 
 def _graph_key(model, x, cal):

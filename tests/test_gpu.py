@@ -234,6 +234,11 @@ def test_conv_limbs_and_edges(gpu, shape, limbs):
     run_conv_case(gpu, cin, cout, k, s, h, limbs=limbs, seed=7 * cin + cout, signed=True, residual=True, relu=True, batch=3)
 
 
+# tile kinds that run only the static-range limb-plane epilogue (fp32 outputs / fp32 residuals /
+# 1-2 limbs: test_gpu_halo.py, test_gpu_resident.py cover them against the LDS-DMA kernel)
+_LEAN_ONLY = (4, 5)  # ops.TILE_HALO3X3, ops.TILE_RESIDENT1X1
+
+
 @pytest.mark.parametrize("limbs", [1, 2, 3])
 @pytest.mark.parametrize("shape", [(64, 256, 1, 1, 20), (128, 128, 3, 2, 17), (64, 80, 3, 1, 9), (256, 48, 1, 1, 7)],
                          ids=lambda s: "c%d_o%d_k%d_s%d_h%d" % s)
@@ -249,7 +254,7 @@ def test_all_tile_configs_bitwise_identical(gpu, shape, limbs):
     shift = torch.linspace(-1, 1, cout, device=gpu)
     outs = []
     for c in ops.tile_configs():  # (the halo kernel runs the lean epilogue only: test_gpu_halo.py)
-        if not ops._tile_fits(c, limbs, 1, cout, cin, k) or ops.tile_kind(c) == ops.TILE_HALO3X3:
+        if not ops._tile_fits(c, limbs, 1, cout, cin, k) or ops.tile_kind(c) in _LEAN_ONLY:
             continue
         ya = torch.zeros(3, device=gpu)
         y = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, residual=res, relu=True,
@@ -287,7 +292,7 @@ def test_static_outputs_identical_across_tiles(gpu, shape, limbs, range_frac):
     rng = float(ref.abs().max()) * range_frac
     outs = []
     for c in ops.tile_configs():
-        if not ops._tile_fits(c, limbs, 1, cout, cin, k) or ops.tile_kind(c) == ops.TILE_HALO3X3:
+        if not ops._tile_fits(c, limbs, 1, cout, cin, k) or ops.tile_kind(c) in _LEAN_ONLY:
             continue
         ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
         y, yq = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, relu=True, tile_cfg=c,
@@ -638,7 +643,7 @@ def test_conv_weight_limbs_vs_emulation(gpu, limbs, wlimbs):
     outs = []
     kinds = set()
     for c in ops.tile_configs():
-        if ops._tile_fits(c, limbs, wlimbs, cout, cin, k) and ops.tile_kind(c) != ops.TILE_HALO3X3:
+        if ops._tile_fits(c, limbs, wlimbs, cout, cin, k) and ops.tile_kind(c) not in _LEAN_ONLY:
             outs.append(ops.conv2d_q(xq, am, codes, None, k, k, s, 1, cs, sh, residual=res, relu=True, tile_cfg=c))
             kinds.add(ops.tile_kind(c))
     assert ops.TILE_LDS_DMA in kinds and ops.TILE_LDS_DMA_K128 in kinds
@@ -1049,7 +1054,7 @@ def test_tile_configs_deterministic(gpu, shape):
     y0, q0 = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, tile_cfg=1, emit_range=rng,
                           overflow=ovf, **kw)
     cfgs = [c for c in ops.tile_configs() if ops._tile_fits(c, limbs, 1, cout, cin, k)
-            and ops.tile_kind(c) != ops.TILE_HALO3X3]  # (fp32 output + residual: not the halo kernel's)
+            and ops.tile_kind(c) not in _LEAN_ONLY]  # (fp32 output + residual: not the halo kernel's)
     for c in cfgs:
         for rep in range(8):
             y, q = ops.conv2d_q(xq, am, codes, offset, k, k, s, k // 2, step, shift, tile_cfg=c, emit_range=rng,
