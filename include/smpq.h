@@ -222,6 +222,29 @@ int smpq_conv2d_pair_fwd(const int8_t* xq, const float* x_absmax, int n, int h, 
                          const float* col_shift2, int8_t* yq2, float yq2_range, int32_t* overflow,
                          smpq_stream_t stream);
 
+/* ABI 7: the general form of the Bottleneck tail chain. conv3 (exact codes; offset1 = its weight
+ * offsets or NULL) with its identity from ONE of
+ *   residual_q / residual_range        the identity's limb planes, as smpq_conv2d_pair_fwd, or
+ *   ds_xq [3][n*h*w][cin], ds_x_absmax [n], ds_codes [3][cout1][cin] (ds_wlimbs = 3: 24-bit fixed
+ *   point from smpq_pack_weights_ex), ds_col_scale / ds_col_shift [cout1], ds_range
+ *                                      the block's 1x1 / stride-1 downsample over the same pixels,
+ *                                      computed in the same tiles: its clamped output codes (what a
+ *                                      smpq_conv2d_fwd_q launch with emit range ds_range writes) are
+ *                                      conv3's residual and are never written; overflow covers them,
+ * and optionally (codes2 != NULL) the next block's conv1 on conv3's output as smpq_conv2d_pair_fwd
+ * (no offsets). Every output and the overflow flag are bitwise those of the separate launches.
+ * Built for conv3 64 -> 256 with cout2 = 64 or no second conv (smpq_conv2d_chain_supported with
+ * cout2 = 0); other calls return SMPQ_E_INVALID. */
+int smpq_conv2d_chain_supported(int cin, int cout1, int cout2, int limbs);
+int smpq_conv2d_chain_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+                          const int8_t* codes1, const int32_t* offset1, int cout1, const float* col_scale1,
+                          const float* col_shift1, const int8_t* residual_q, float residual_range,
+                          const int8_t* ds_xq, const float* ds_x_absmax, const int8_t* ds_codes, int ds_wlimbs,
+                          const float* ds_col_scale, const float* ds_col_shift, float ds_range, int8_t* yq1,
+                          float yq1_range, const float* y1_absmax, const int8_t* codes2, int cout2,
+                          const float* col_scale2, const float* col_shift2, int8_t* yq2, float yq2_range,
+                          int32_t* overflow, smpq_stream_t stream);
+
 /* codes [wlimbs][cout][K] (K % 64 == 0, 16-B aligned) -> out [wlimbs][K/64][cout][64], the K-major
  * copy smpq_conv2d_fwd_q_km reads. */
 int smpq_weights_kmajor(const int8_t* codes, int wlimbs, int cout, int K, int8_t* out, smpq_stream_t stream);
@@ -301,13 +324,14 @@ int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads);
  *                              (TH x TW of one image), BN = 64.
  *   SMPQ_TILE_RESIDENT1X1      (ABI 6) weight-stationary 1x1 tiles: 1x1 / pad 0 convs with cin
  *                              64 .. 1024 (per configuration: smpq_conv2d_tile_supported), cout a
- *                              multiple of the slab (BN = 64 / 128 / 256), 3 activation limbs, no
- *                              weight offsets, static-range limb-plane output (yq set; y, y_absmax,
- *                              residual NULL); 3 weight limbs without ReLU or residual_q (the
- *                              downsamples), 1 weight limb with ReLU and optionally residual_q, or
- *                              neither — other calls return SMPQ_E_INVALID. A persistent workgroup
- *                              keeps its slab's weight limbs in registers and walks pixel tiles;
- *                              BM = pixels per tile, BN = the slab. Configurations follow the halo ones.
+ *                              multiple of the slab (BN = 64 / 128 / 256), 3 activation limbs,
+ *                              static-range limb-plane output (yq set; y, y_absmax, residual NULL);
+ *                              3 weight limbs without ReLU or residual_q (the downsamples), 1 weight
+ *                              limb with ReLU and optionally residual_q (both with or without weight
+ *                              offsets), or neither (no offsets) — other calls return
+ *                              SMPQ_E_INVALID. A persistent workgroup keeps its slab's weight limbs
+ *                              in registers and walks pixel tiles; BM = pixels per tile, BN = the
+ *                              slab. Configurations follow the halo ones.
  * (negative: error code). Values 0 and 1 were the register-staged family (ABI <= 3, removed). */
 #define SMPQ_TILE_LDS_DMA 2
 #define SMPQ_TILE_LDS_DMA_K128 3

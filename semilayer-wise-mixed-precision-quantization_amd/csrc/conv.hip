@@ -634,7 +634,50 @@ extern "C" int smpq_debug_mfma_i8(const int8_t* a, const int8_t* b, int32_t* c, 
 }
 
 extern "C" int smpq_conv2d_pair_supported(int cin, int cout1, int cout2, int limbs) {
+  return cout2 > 0 && resident_pair_supported(cin, cout1, cout2, limbs) ? 1 : 0;
+}
+
+extern "C" int smpq_conv2d_chain_supported(int cin, int cout1, int cout2, int limbs) {
   return resident_pair_supported(cin, cout1, cout2, limbs) ? 1 : 0;
+}
+
+extern "C" int smpq_conv2d_chain_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
+                                     const int8_t* codes1, const int32_t* offset1, int cout1, const float* col_scale1,
+                                     const float* col_shift1, const int8_t* residual_q, float residual_range,
+                                     const int8_t* ds_xq, const float* ds_x_absmax, const int8_t* ds_codes,
+                                     int ds_wlimbs, const float* ds_col_scale, const float* ds_col_shift,
+                                     float ds_range, int8_t* yq1, float yq1_range, const float* y1_absmax,
+                                     const int8_t* codes2, int cout2, const float* col_scale2,
+                                     const float* col_shift2, int8_t* yq2, float yq2_range, int32_t* overflow,
+                                     smpq_stream_t stream) {
+  constexpr int limbs = 3;
+  if (!yq1 || (!residual_q) == (!ds_xq)) return fail(SMPQ_E_INVALID, "smpq_conv2d_chain_fwd: yq1 and exactly one "
+                                                                      "identity source (residual_q or ds_xq)");
+  if (ds_xq && (!ds_x_absmax || !ds_codes || ds_wlimbs != 3 || !(ds_range > 0.f)))
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_chain_fwd: the fused downsample needs its input range, 3-limb "
+                                "weights and a positive output range");
+  if (codes2 && (!yq2 || !y1_absmax)) return fail(SMPQ_E_INVALID, "smpq_conv2d_chain_fwd: null pointer");
+  ConvArgs a, b, d;
+  // conv3; with a fused downsample its residual is the downsample's codes at scale ds_range / QMAX
+  int rc = conv_args_q(xq, x_absmax, n, h, w, cin, codes1, 1, offset1, cout1, 1, 1, 1, 0, col_scale1, col_shift1,
+                       nullptr, 1, limbs, nullptr, nullptr, yq1, yq1_range, overflow, residual_q, residual_range, a);
+  if (rc) return rc;
+  if (ds_xq) {
+    a.res_scale = ds_range / 8323072.f;
+    // the downsample as its own launch would run it (its output quantizer: yq1 stands in for the
+    // planes it would write; the chain never writes them)
+    rc = conv_args_q(ds_xq, ds_x_absmax, n, h, w, cin, ds_codes, 3, nullptr, cout1, 1, 1, 1, 0, ds_col_scale,
+                     ds_col_shift, nullptr, 0, limbs, nullptr, nullptr, yq1, ds_range, overflow, nullptr, 0.f, d);
+    if (rc) return rc;
+  }
+  if (codes2) {
+    rc = conv_args_q(yq1, y1_absmax, n, h, w, cout1, codes2, 1, nullptr, cout2, 1, 1, 1, 0, col_scale2, col_shift2,
+                     nullptr, 1, limbs, nullptr, nullptr, yq2, yq2_range, overflow, nullptr, 0.f, b);
+    if (rc) return rc;
+  }
+  const long long big = (long long)limbs * a.M * (cout1 > cin ? cout1 : cin);
+  if (big > 0x7fffff00LL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_chain_fwd: a limb plane of 2 GiB or more");
+  return launch_resident_chain(a, codes2 ? &b : nullptr, ds_xq ? &d : nullptr, limbs, (hipStream_t)stream);
 }
 
 extern "C" int smpq_conv2d_pair_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
@@ -643,18 +686,8 @@ extern "C" int smpq_conv2d_pair_fwd(const int8_t* xq, const float* x_absmax, int
                                     int8_t* yq1, float yq1_range, const float* y1_absmax, const int8_t* codes2,
                                     int cout2, const float* col_scale2, const float* col_shift2, int8_t* yq2,
                                     float yq2_range, int32_t* overflow, smpq_stream_t stream) {
-  constexpr int limbs = 3;
-  if (!yq1 || !yq2 || !residual_q || !y1_absmax)
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_pair_fwd: null pointer");
-  ConvArgs a, b;
-  int rc = conv_args_q(xq, x_absmax, n, h, w, cin, codes1, 1, nullptr, cout1, 1, 1, 1, 0, col_scale1, col_shift1,
-                       nullptr, 1, limbs, nullptr, nullptr, yq1, yq1_range, overflow, residual_q, residual_range, a);
-  if (rc) return rc;
-  // the second conv reads the first one's output planes: as a separate launch, on yq1 with y1_absmax
-  rc = conv_args_q(yq1, y1_absmax, n, h, w, cout1, codes2, 1, nullptr, cout2, 1, 1, 1, 0, col_scale2, col_shift2,
-                   nullptr, 1, limbs, nullptr, nullptr, yq2, yq2_range, overflow, nullptr, 0.f, b);
-  if (rc) return rc;
-  const long long big = (long long)limbs * a.M * (cout1 > cin ? cout1 : cin);
-  if (big > 0x7fffff00LL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_pair_fwd: a limb plane of 2 GiB or more");
-  return launch_resident_pair(a, b, limbs, (hipStream_t)stream);
+  if (!residual_q || !codes2) return fail(SMPQ_E_INVALID, "smpq_conv2d_pair_fwd: null pointer");
+  return smpq_conv2d_chain_fwd(xq, x_absmax, n, h, w, cin, codes1, nullptr, cout1, col_scale1, col_shift1, residual_q,
+                               residual_range, nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0.f, yq1, yq1_range,
+                               y1_absmax, codes2, cout2, col_scale2, col_shift2, yq2, yq2_range, overflow, stream);
 }

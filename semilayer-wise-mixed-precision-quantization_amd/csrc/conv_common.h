@@ -100,9 +100,9 @@ void resident_cfg_info(int cfg, int* bm, int* bn, int* threads);
 bool resident_supported(int cfg, int cin, int cout, int kh, int kw, int limbs, int wlimbs);
 int launch_resident(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s);
 bool glds_is_resident(int cfg);
-// the chained conv3 -> next conv1 pair of the Bottlenecks (smpq_conv2d_pair_fwd)
+// the Bottleneck tail chains: conv3 (+ fused downsample) (-> next conv1) (smpq_conv2d_chain_fwd)
 bool resident_pair_supported(int cin, int cout1, int cout2, int limbs);
-int launch_resident_pair(const ConvArgs& a, const ConvArgs& b, int limbs, hipStream_t s);
+int launch_resident_chain(const ConvArgs& a, const ConvArgs* b, const ConvArgs* d, int limbs, hipStream_t s);
 
 // The 4 codes (channels 0..3) held by one dword per limb plane, w[l] = the 4 balanced digits of
 // limb l: q = sum_l d_l 256^l. With u_l = d_l + 128 (byte ^ 0x80) for the low limbs,

@@ -31,6 +31,18 @@
 // fragments), and conv1's own [L][BP][64 CW2] tile is staged and copied out beside it. Both outputs
 // are bitwise those of the two separate launches (the same codes, the same epilogue); conv1's
 // activation read from HBM disappears.
+//
+// Fused downsample (LWD > 0): in the first block of a stage the identity conv3 adds is the
+// downsample's output (resnet.py:108-113 with :188-192), written as limb planes by one launch and
+// read back by conv3. Where the downsample is a 1x1 / stride-1 conv over the same pixels and K as
+// conv3 (the R50 layer1 block 0: 64 -> 256 at 56^2), its activation tile arrives beside conv3's, its
+// 24-bit fixed-point weight limbs sit in VGPRs too, and its epilogue's clamped codes (the values its
+// own launch would have written) feed conv3's residual directly: both HBM round trips of the
+// downsample output and its launch disappear; the overflow flag covers both outputs.
+//
+// Weight offsets (OFF; exact-code channels whose codes sit off-centre): acc_l += offset_c * (sum of
+// the pixel's limb-l digits), the digit sums taken with v_dot4 on the B fragments — the LDS-DMA
+// kernel's exact integer correction.
 #include "conv_common.h"
 #include "lds_dma.h"
 
@@ -53,6 +65,11 @@ constexpr ResCfg kRes[] = {
 constexpr bool res_fits(int lw, int kc, int cw) { return lw * kc * cw <= 32; }
 constexpr int kNumRes = sizeof(kRes) / sizeof(kRes[0]);
 constexpr int kResThreads = 256;
+// Per-image input scales staged in LDS at the start (up to kNTab images; more: read from memory).
+// A global load inside the tile loop would end in an s_waitcnt vmcnt the compiler places for it —
+// which also waits for the next tile's activation DMA and the copy-out stores issued before it,
+// serialising every tile on a full memory round trip.
+constexpr int kNTab = 256;
 
 // the 16-B chunk c of activation row r is stored at chunk ach<KC>(c, r): conflict-free DMA writes and
 // fragment reads (16 rows, chunk fixed per lane group) for 64-B rows (KC = 1, the LDS-DMA kernel's
@@ -64,29 +81,43 @@ __device__ __forceinline__ int ach(int c, int r) {
   else return c ^ (r & 15);
 }
 
-template <int L, int LW, int KC, int CW, int WP, bool RES, int CW2 = 0>
+template <int L, int LW, int KC, int CW, int WP, bool RES, int CW2 = 0, int LWD = 0, bool OFF = false>
 struct ResShape {
   static constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
   static constexpr int NACC = L + LW - 1 - SMIN;
   static constexpr int BN = 64 * CW, BP = 16 * WP, K = 64 * KC;
-  static constexpr int ASTAGE = L * BP * K;  // activation tile bytes
+  static constexpr int ATILE = L * BP * K;                     // activation tile bytes
+  static constexpr int ASTAGE = ATILE * (LWD > 0 ? 2 : 1);     // + the fused downsample's tile
   static constexpr int OTILE = L * BP * BN;  // output (and residual) tile bytes
   static constexpr int OTILE2 = L * BP * 64 * CW2;  // the chained conv's output tile
   static constexpr int LDS = 2 * ASTAGE + (RES ? 3 : 1) * OTILE + OTILE2;
   // VGPRs: weights (+ the chained conv's) + accumulators + one chunk's B fragments + addressing /
   // epilogue (~40)
-  static constexpr int REGS = 4 * (LW * KC * CW + CW * CW2 + NACC * CW * WP + L * WP) + 40;
+  // (+ the fused downsample's accumulators and epilogue constants; the offsets and digit sums: the
+  // compiler's counts, tools/ resource usage, need this much margin to stay spill-free)
+  static constexpr int NACC_D = LWD > 0 ? L + LWD - 1 - ((L + LWD - 4) > 0 ? (L + LWD - 4) : 0) : 0;
+  static constexpr int REGS = 4 * (LW * KC * CW + CW * CW2 + LWD * KC * CW + NACC * CW * WP + L * WP) + 40 +
+                              (LWD > 0 ? 8 * CW + 4 * CW * WP + (CW2 > 0 ? 4 * NACC_D * CW * WP : 0) : 0) +
+                              (OFF ? 8 * CW + L * WP : 0);
   // workgroups per CU (1 wave per SIMD each; past 256 the accumulators move to AGPRs)
-  static constexpr int MINW_R = REGS <= 128 ? 4 : (REGS <= 160 ? 3 : (REGS <= 240 ? 2 : 1));
-  static constexpr int MINW_L = (160 * 1024) / LDS;
+  static constexpr int MINW_R = REGS <= 120 ? 4 : (REGS <= 152 ? 3 : (REGS <= 240 ? 2 : 1));
+  // + the per-image input scales (x_absmax / QMAX) of each conv, staged once (kNTab images)
+  static constexpr int NTABS = 1 + (LWD > 0 ? 1 : 0) + (CW2 > 0 ? 1 : 0);
+  static constexpr int LDS_TOTAL = LDS + NTABS * kNTab * 4;
+  static constexpr int MINW_L = (160 * 1024) / LDS_TOTAL;
   static constexpr int MINW = MINW_R < MINW_L ? MINW_R : MINW_L;
 };
 
-template <int L, int LW, int KC, int CW, int WP, bool RELU, bool RES, int MINW, int CW2 = 0>
-__global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvArgs a, ConvArgs b, int ntiles,
-                                                                           int nslabs) {
-  using S = ResShape<L, LW, KC, CW, WP, RES, CW2>;
+template <int L, int LW, int KC, int CW, int WP, bool RELU, bool RES, int MINW, int CW2 = 0, bool OFF = false,
+          int LWD = 0>
+__global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvArgs a, ConvArgs b, ConvArgs d,
+                                                                           int ntiles, int nslabs) {
+  using S = ResShape<L, LW, KC, CW, WP, RES, CW2, LWD, OFF>;
   constexpr int SMIN = S::SMIN, NACC = S::NACC, BN = S::BN, BP = S::BP, K = S::K, ASTAGE = S::ASTAGE;
+  constexpr int ATILE = S::ATILE;
+  static_assert(!OFF || (LW == 1 && SMIN == 0), "weight offsets: exact codes only");
+  static_assert(!(RES && LWD > 0), "one residual source");
+  constexpr int SMIN_D = (L + LWD - 4) > 0 ? (L + LWD - 4) : 0, NACC_D = LWD > 0 ? L + LWD - 1 - SMIN_D : 1;
   constexpr int CH = K / 16;       // 16-B chunks per activation row
   constexpr int RP = 1024 / K;     // activation rows per 1-KiB DMA piece
   constexpr int APIECES = L * BP / RP;
@@ -99,6 +130,16 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
   int8_t* const otile = lds + 2 * ASTAGE;
   constexpr int OTILE = S::OTILE;
   const unsigned rtile0 = lds0 + 2 * ASTAGE + OTILE;  // residual tile of stage s at rtile0 + s OTILE
+  // per-image scales: [0] this conv's input, [1] the fused downsample's, [2] the chained conv's
+  float* const rtab = reinterpret_cast<float*>(lds + S::LDS);
+  const bool tab_ok = a.n <= kNTab;
+  if (tab_ok) {
+    for (int i = threadIdx.x; i < a.n; i += kResThreads) {
+      rtab[i] = a.x_absmax[i] * a.inv_qmax;
+      if constexpr (LWD > 0) rtab[kNTab + i] = d.x_absmax[i] * d.inv_qmax;
+      if constexpr (CW2 > 0) rtab[(S::NTABS - 1) * kNTab + i] = b.x_absmax[i] * b.inv_qmax;
+    }
+  }  // (visible to every wave after the tile loop's first barrier)
   const int slab = blockIdx.x % nslabs;
   const int n0 = slab * BN;
   const int tstride = gridDim.x / nslabs;
@@ -134,14 +175,35 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
         wb[kc][i] = v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
       }
   }
+  // the fused downsample's weight limbs (LWD > 0: same slab, same K)
+  v4i wd[LWD > 0 ? LWD : 1][LWD > 0 ? KC : 1][LWD > 0 ? CW : 1];
+  if constexpr (LWD > 0) {
+    const auto wrsd = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(d.codes), 0, (int)(LWD * d.wplane), 0x00020000);
+#pragma unroll
+    for (int lw = 0; lw < LWD; ++lw)
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+        for (int i = 0; i < CW; ++i) {
+          const int row = n0 + (wave * CW + i) * 16 + frow;
+          const unsigned off = d.w_kmajor ? (unsigned)(kc * d.cout * 64 + row * 64 + 16 * grp)
+                                          : (unsigned)(row * K + kc * 64 + 16 * grp);
+          const v4u v = __builtin_amdgcn_raw_buffer_load_b128(wrsd, off, (unsigned)(lw * d.wplane), 0);
+          wd[lw][kc][i] = v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+        }
+  }
 
   // ---- activation DMA: piece = RP pixel rows x K bytes of one limb; lane -> (row, physical chunk)
   const int prow = lane / CH, pphys = lane % CH;
   const v4i xrs = make_rsrc(a.xq, (long long)L * a.plane);
+  const v4i xrsd = make_rsrc(LWD > 0 ? d.xq : nullptr, LWD > 0 ? (long long)L * d.plane : 0);
   const int hw_out = a.ho * a.wo;
   auto issue_acts = [&](int t, int stage) {
-    for (int p = wave; p < APIECES; p += 4) {
-      const int l = p / (BP / RP), r = (p % (BP / RP)) * RP + prow;  // tile row (pixel) of this lane
+    for (int p = wave; p < (LWD > 0 ? 2 : 1) * APIECES; p += 4) {
+      // pieces APIECES.. : the fused downsample's tile (the same pixels, addressing and K)
+      const bool dsp = LWD > 0 && p >= APIECES;
+      const int pp = dsp ? p - APIECES : p;
+      const int l = pp / (BP / RP), r = (pp % (BP / RP)) * RP + prow;  // tile row (pixel) of this lane
       const int m = t * BP + r;
       unsigned src = kOOB;
       if (m < a.M) {
@@ -150,7 +212,11 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
         const int oh = fast_div(rem, a.wo_mul, a.wo_shr), ow = rem - oh * a.wo;
         src = (unsigned)(((img * a.h + oh * a.stride) * a.w + ow * a.stride) * K + 16 * ach<KC>(pphys, r));
       }
-      dma16(lds0 + stage * ASTAGE + p * 1024, xrs, src, __builtin_amdgcn_readfirstlane((unsigned)((long long)l * a.plane)));
+      if (dsp)
+        dma16(lds0 + stage * ASTAGE + ATILE + pp * 1024, xrsd, src,
+              __builtin_amdgcn_readfirstlane((unsigned)((long long)l * d.plane)));
+      else
+        dma16(lds0 + stage * ASTAGE + p * 1024, xrs, src, __builtin_amdgcn_readfirstlane((unsigned)((long long)l * a.plane)));
     }
   };
   // the residual tile [L][BP][BN] of tile t (RES): piece = 1024 / BN rows x BN bytes of one limb, 16-B
@@ -189,6 +255,27 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
   }
   const float lo = RELU ? 0.f : -qmax;
   const float rsq = a.res_scale * inv;
+  // the fused downsample's epilogue constants, and this lane's weight offsets
+  float csqd[LWD > 0 ? CW : 1][4], shqd[LWD > 0 ? CW : 1][4];
+  if constexpr (LWD > 0) {
+    const float invd = d.yq_inv;
+#pragma unroll
+    for (int i = 0; i < CW; ++i) {
+      const int c = n0 + (wave * CW + i) * 16 + 4 * grp;
+      const float4 cs = *reinterpret_cast<const float4*>(d.col_scale + c);
+      const float4 csh = *reinterpret_cast<const float4*>(d.col_shift + c);
+      csqd[i][0] = cs.x * invd, csqd[i][1] = cs.y * invd, csqd[i][2] = cs.z * invd, csqd[i][3] = cs.w * invd;
+      shqd[i][0] = csh.x * invd, shqd[i][1] = csh.y * invd, shqd[i][2] = csh.z * invd, shqd[i][3] = csh.w * invd;
+    }
+  }
+  int woff[OFF ? CW : 1][4];
+  if constexpr (OFF) {
+#pragma unroll
+    for (int i = 0; i < CW; ++i) {
+      const int4 o = *reinterpret_cast<const int4*>(a.w_off + n0 + (wave * CW + i) * 16 + 4 * grp);
+      woff[i][0] = o.x, woff[i][1] = o.y, woff[i][2] = o.z, woff[i][3] = o.w;
+    }
+  }
   const v4i qrs4 = make_rsrc(a.yq, (long long)L * oplane);
   // the chained conv's epilogue constants, output planes and staged tile
   const float inv2 = CW2 > 0 ? b.yq_inv : 0.f;
@@ -265,6 +352,66 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
       for (int i = 0; i < CW; ++i)
 #pragma unroll
         for (int j = 0; j < WP; ++j) acc[s][i][j] = v4i{0, 0, 0, 0};
+    v4i accd[NACC_D][LWD > 0 ? CW : 1][LWD > 0 ? WP : 1];
+    if constexpr (LWD > 0) {
+#pragma unroll
+      for (int s = 0; s < NACC_D; ++s)
+#pragma unroll
+        for (int i = 0; i < CW; ++i)
+#pragma unroll
+          for (int j = 0; j < WP; ++j) accd[s][i][j] = v4i{0, 0, 0, 0};
+    }
+    // the fused downsample first: its MFMAs, then its epilogue's clamped codes (conv3's residual),
+    // so that its accumulators are dead before conv3's are live
+    int dq[LWD > 0 ? CW : 1][LWD > 0 ? WP : 1][4];
+    if constexpr (LWD > 0) {
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        v4i fd[L][WP];
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+#pragma unroll
+          for (int j = 0; j < WP; ++j) {
+            const int r = j * 16 + frow;
+            fd[l][j] = *reinterpret_cast<const v4i*>(as + ATILE + (l * BP + r) * K + 16 * ach<KC>(4 * kc + grp, r));
+          }
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+#pragma unroll
+          for (int lw = 0; lw < LWD; ++lw) {
+            if (l + lw < SMIN_D) continue;
+#pragma unroll
+            for (int i = 0; i < CW; ++i)
+#pragma unroll
+              for (int j = 0; j < WP; ++j)
+                accd[l + lw - SMIN_D][i][j] =
+                    __builtin_amdgcn_mfma_i32_16x16x64_i8(wd[lw][kc][i], fd[l][j], accd[l + lw - SMIN_D][i][j], 0, 0, 0);
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < WP; ++j) {
+        const int m = m0 + j * 16 + frow;
+        const int img = m < a.M ? fast_div(m, a.hw_mul, a.hw_shr) : 0;
+        const float rscd = m < a.M ? (tab_ok ? rtab[kNTab + img] : d.x_absmax[img] * d.inv_qmax) : 0.f;
+#pragma unroll
+        for (int i = 0; i < CW; ++i) {
+          v4i accqd[NACC_D];
+#pragma unroll
+          for (int s2 = 0; s2 < NACC_D; ++s2) accqd[s2] = accd[s2][i][j];
+          const int rq0[4] = {0, 0, 0, 0};
+          const float md = lean_codes<L, NACC_D, SMIN_D>(accqd, rscd, csqd[i], shqd[i], false, rq0, 0.f, false, -qmax,
+                                                         dq[i][j]);
+          vmax = m < a.M ? fmaxf(vmax, md) : vmax;
+        }
+      }
+    }
+    int rs[OFF ? L : 1][OFF ? WP : 1];  // digit sums of this lane's 16-B slices (OFF)
+    if constexpr (OFF) {
+#pragma unroll
+      for (int l = 0; l < L; ++l)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) rs[l][j] = 0;
+    }
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       v4i fb[L][WP];
@@ -275,6 +422,19 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
           const int r = j * 16 + frow;
           fb[l][j] = *reinterpret_cast<const v4i*>(as + (l * BP + r) * K + 16 * ach<KC>(4 * kc + grp, r));
         }
+      if constexpr (OFF) {
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+#pragma unroll
+          for (int j = 0; j < WP; ++j) {
+            int sdig = rs[l][j];
+            sdig = __builtin_amdgcn_sdot4(fb[l][j].x, 0x01010101, sdig, false);
+            sdig = __builtin_amdgcn_sdot4(fb[l][j].y, 0x01010101, sdig, false);
+            sdig = __builtin_amdgcn_sdot4(fb[l][j].z, 0x01010101, sdig, false);
+            sdig = __builtin_amdgcn_sdot4(fb[l][j].w, 0x01010101, sdig, false);
+            rs[l][j] = sdig;
+          }
+      }
 #pragma unroll
       for (int l = 0; l < L; ++l)
 #pragma unroll
@@ -288,6 +448,27 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
                   __builtin_amdgcn_mfma_i32_16x16x64_i8(wa[lw][kc][i], fb[l][j], acc[l + lw - SMIN][i][j], 0, 0, 0);
         }
     }
+    if constexpr (OFF) {
+      // whole-row digit sums (the 4 lane groups hold 16 B each), then acc_l += offset_c * sum_l: the
+      // LDS-DMA kernel's integer correction (|offset| < 2^15, |sum| < 2^22: exact 24-bit products)
+#pragma unroll
+      for (int l = 0; l < L; ++l)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+          int sdig = rs[l][j];
+          sdig += __shfl_xor(sdig, 16, 64);
+          sdig += __shfl_xor(sdig, 32, 64);
+          rs[l][j] = sdig;
+        }
+#pragma unroll
+      for (int i = 0; i < CW; ++i)
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+#pragma unroll
+          for (int j = 0; j < WP; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[l][i][j][r] += __mul24(woff[i][r], rs[l][j]);
+    }
     // every wave's copy-out reads of the staged output tile are done before it is overwritten
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -297,7 +478,8 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
 #pragma unroll
     for (int j = 0; j < WP; ++j) {
       const int m = m0 + j * 16 + frow;
-      const float rscale = m < a.M ? a.x_absmax[fast_div(m, a.hw_mul, a.hw_shr)] * a.inv_qmax : 0.f;
+      const int img = m < a.M ? fast_div(m, a.hw_mul, a.hw_shr) : 0;
+      const float rscale = m < a.M ? (tab_ok ? rtab[img] : a.x_absmax[img] * a.inv_qmax) : 0.f;
 #pragma unroll
       for (int i = 0; i < CW; ++i) {
         v4i accq[NACC];
@@ -305,6 +487,10 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
         for (int s = 0; s < NACC; ++s) accq[s] = acc[s][i][j];
         const int rt = j * 16 + frow, cc = wave * CW + i;
         int rqv[4] = {0, 0, 0, 0};
+        if constexpr (LWD > 0) {  // the downsample's clamped output codes (what its own launch writes)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rqv[r] = dq[i][j][r];
+        }
         if constexpr (RES) {
           unsigned rw[L];
 #pragma unroll
@@ -314,7 +500,7 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
           decode4<L>(rw, rqv);
         }
         unsigned wq[L];
-        const float mm = lean_quad<L, NACC, SMIN>(accq, rscale, csq[i], shq[i], RES, rqv, rsq, RELU, lo, wq);
+        const float mm = lean_quad<L, NACC, SMIN>(accq, rscale, csq[i], shq[i], RES || LWD > 0, rqv, rsq, RELU, lo, wq);
         vmax = m < a.M ? fmaxf(vmax, mm) : vmax;
 #pragma unroll
         for (int l = 0; l < L; ++l)
@@ -355,7 +541,9 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
 #pragma unroll
       for (int j = 0; j < WP; ++j) {
         const int m = m0 + j * 16 + frow;
-        const float rscale = m < a.M ? b.x_absmax[fast_div(m, a.hw_mul, a.hw_shr)] * b.inv_qmax : 0.f;
+        const int img = m < a.M ? fast_div(m, a.hw_mul, a.hw_shr) : 0;
+        const float rscale =
+            m < a.M ? (tab_ok ? rtab[(S::NTABS - 1) * kNTab + img] : b.x_absmax[img] * b.inv_qmax) : 0.f;
 #pragma unroll
         for (int i = 0; i < CW2; ++i) {
           v4i accq[L];
@@ -396,18 +584,18 @@ int device_cus_res() {
   return cus;
 }
 
-template <int L, int LW, int CFG, int KC, bool RELU, bool RES>
+template <int L, int LW, int CFG, int KC, bool RELU, bool RES, bool OFF>
 int launch_res_one(const ConvArgs& a, hipStream_t s) {
   constexpr int CW = kRes[CFG].cw, WP = kRes[CFG].wp;
   if constexpr (!((kRes[CFG].kc_mask >> KC) & 1) || !res_fits(LW, KC, CW)) {
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tile: cin not built for this configuration");
   } else {
-  using S = ResShape<L, LW, KC, CW, WP, RES>;
+  using S = ResShape<L, LW, KC, CW, WP, RES, 0, 0, OFF>;
   static_assert(S::MINW >= 1, "LDS per CU");
-  auto k = qconv_resident_kernel<L, LW, KC, CW, WP, RELU, RES, S::MINW>;
+  auto k = qconv_resident_kernel<L, LW, KC, CW, WP, RELU, RES, S::MINW, 0, OFF>;
   static const hipError_t attr = [&] {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS_TOTAL);
     if (e != hipSuccess) (void)hipGetLastError();
     return e;
   }();
@@ -421,53 +609,57 @@ int launch_res_one(const ConvArgs& a, hipStream_t s) {
   if (per_slab < 1) per_slab = 1;
   if (per_slab > ntiles) per_slab = ntiles;
   const long long blocks = per_slab * nslabs;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kResThreads), S::LDS, s, a, a, (int)ntiles, nslabs);
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kResThreads), S::LDS_TOTAL, s, a, a, a, (int)ntiles, nslabs);
   return check_hip(hipGetLastError(), "qconv_resident_kernel launch");
   }
 }
 
-template <int L, int LW, int CFG, bool RELU, bool RES>
+template <int L, int LW, int CFG, bool RELU, bool RES, bool OFF>
 int launch_res_kc(int kc, const ConvArgs& a, hipStream_t s) {
   switch (kc) {  // only the K sizes of the configuration's mask are instantiated
-    case 1: return launch_res_one<L, LW, CFG, 1, RELU, RES>(a, s);
-    case 2: return launch_res_one<L, LW, CFG, 2, RELU, RES>(a, s);
-    case 4: return launch_res_one<L, LW, CFG, 4, RELU, RES>(a, s);
-    case 8: return launch_res_one<L, LW, CFG, 8, RELU, RES>(a, s);
-    case 16: return launch_res_one<L, LW, CFG, 16, RELU, RES>(a, s);
+    case 1: return launch_res_one<L, LW, CFG, 1, RELU, RES, OFF>(a, s);
+    case 2: return launch_res_one<L, LW, CFG, 2, RELU, RES, OFF>(a, s);
+    case 4: return launch_res_one<L, LW, CFG, 4, RELU, RES, OFF>(a, s);
+    case 8: return launch_res_one<L, LW, CFG, 8, RELU, RES, OFF>(a, s);
+    case 16: return launch_res_one<L, LW, CFG, 16, RELU, RES, OFF>(a, s);
     default: return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tile: cin not built");
   }
 }
 
-template <int L, int LW, bool RELU, bool RES>
+template <int L, int LW, bool RELU, bool RES, bool OFF = false>
 int launch_res_l(int cfg, const ConvArgs& a, hipStream_t s) {
   const int kc = a.cin / 64;
   switch (cfg) {
-    case 0: return launch_res_kc<L, LW, 0, RELU, RES>(kc, a, s);
-    case 1: return launch_res_kc<L, LW, 1, RELU, RES>(kc, a, s);
-    case 2: return launch_res_kc<L, LW, 2, RELU, RES>(kc, a, s);
-    default: return launch_res_kc<L, LW, 3, RELU, RES>(kc, a, s);
+    case 0: return launch_res_kc<L, LW, 0, RELU, RES, OFF>(kc, a, s);
+    case 1: return launch_res_kc<L, LW, 1, RELU, RES, OFF>(kc, a, s);
+    case 2: return launch_res_kc<L, LW, 2, RELU, RES, OFF>(kc, a, s);
+    default: return launch_res_kc<L, LW, 3, RELU, RES, OFF>(kc, a, s);
   }
 }
 
-// the chained pair (CW2 > 0): one slab with all of the first conv's output channels, 16-pixel tiles
-template <int L, int KC, int CW, int CW2>
-int launch_pair_one(const ConvArgs& a, const ConvArgs& b, hipStream_t s) {
-  using S = ResShape<L, 1, KC, CW, 1, true, CW2>;
+// the Bottleneck tail chain: conv3 (one slab with all its output channels, 16-pixel tiles) with
+// its identity as limb planes (LWD == 0) or as the fused downsample (LWD == 3), optionally the next
+// block's conv1 (CW2 > 0), conv3's weight offsets or not
+template <int L, int KC, int CW, int CW2, bool OFF, int LWD>
+int launch_chain_one(const ConvArgs& a, const ConvArgs& b, const ConvArgs& d, hipStream_t s) {
+  using S = ResShape<L, 1, KC, CW, 1, LWD == 0, CW2, LWD, OFF>;
   static_assert(S::MINW >= 1, "LDS per CU");
-  auto k = qconv_resident_kernel<L, 1, KC, CW, 1, true, true, S::MINW, CW2>;
+  auto k = qconv_resident_kernel<L, 1, KC, CW, 1, true, LWD == 0, S::MINW, CW2, OFF, LWD>;
   static const hipError_t attr = [&] {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS_TOTAL);
     if (e != hipSuccess) (void)hipGetLastError();
     return e;
   }();
-  if (attr != hipSuccess) return check_hip(attr, "qconv_resident_kernel (pair) LDS attribute");
+  if (attr != hipSuccess) return check_hip(attr, "qconv_resident_kernel (chain) LDS attribute");
   const long long ntiles = ((long long)a.M + S::BP - 1) / S::BP;
-  long long blocks = (long long)device_cus_res() * S::MINW;
-  if (blocks > ntiles) blocks = ntiles;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kResThreads), S::LDS, s, a, b, (int)ntiles, 1);
-  return check_hip(hipGetLastError(), "qconv_resident_kernel (pair) launch");
+  const int nslabs = a.cout / S::BN;  // 1 with a chained conv (it needs every channel of the tile)
+  long long per_slab = (long long)device_cus_res() * S::MINW / nslabs;
+  if (per_slab > ntiles) per_slab = ntiles;
+  if (per_slab < 1) per_slab = 1;
+  hipLaunchKernelGGL(k, dim3((unsigned)(per_slab * nslabs)), dim3(kResThreads), S::LDS_TOTAL, s, a, b, d, (int)ntiles,
+                     nslabs);
+  return check_hip(hipGetLastError(), "qconv_resident_kernel (chain) launch");
 }
 
 }  // namespace
@@ -493,9 +685,14 @@ int launch_resident(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream
   if (!resident_supported(cfg, a.cin, a.cout, a.kh, a.kw, limbs, wlimbs) || a.pad != 0 || a.s2d)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tiles take 1x1 / pad 0 convs with 3 activation limbs, "
                                 "1 or 3 weight limbs and the tile's cin (64 .. 1024) and slab of couts");
-  if (!a.yq || a.y || a.residual || a.y_absmax || a.has_offset)
+  if (!a.yq || a.y || a.residual || a.y_absmax)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tiles run the static-range limb-plane epilogue (with a "
-                                "limb-plane residual or none) without weight offsets only");
+                                "limb-plane residual or none) only");
+  if (a.has_offset) {  // exact codes off-centre (ReLU convs: conv1 / conv3)
+    if (wlimbs != 1 || !a.relu)
+      return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: resident tiles with weight offsets: one weight limb and ReLU");
+    return a.res_q ? launch_res_l<3, 1, true, true, true>(cfg, a, s) : launch_res_l<3, 1, true, false, true>(cfg, a, s);
+  }
   // built variants: the downsamples (3 weight limbs, no ReLU, no residual), conv1 / conv2 (ReLU), conv3
   // (ReLU + limb-plane residual) and plain (neither)
   if (wlimbs == 3) {
@@ -510,24 +707,41 @@ int launch_resident(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream
   return a.relu ? launch_res_l<3, 1, true, false>(cfg, a, s) : launch_res_l<3, 1, false, false>(cfg, a, s);
 }
 
-// Bottleneck conv3 (+ limb-plane identity, ReLU) chained with the next block's conv1 (ReLU):
-// (cin, cout1, cout2) = (64, 256, 64), the R50 layer1 blocks. (The layer2 chain 128 -> 512 -> 128,
+// Bottleneck conv3 (+ identity, ReLU) chained with the next block's conv1 (ReLU; cout2 = 0: none)
+// and / or its fused downsample: (cin, cout1, cout2) = (64, 256, 64 or 0), the R50 layer1 blocks. (The
+// layer2 chain 128 -> 512 -> 128,
 // one 512-channel slab: 452 registers per lane, one workgroup per CU, measured 0.82-0.85x the two
 // launches and the R50 step 1.2 % slower: profiles/r06_pair_chain.txt; not built.)
 bool resident_pair_supported(int cin, int cout1, int cout2, int limbs) {
-  return limbs == 3 && cin == 64 && cout1 == 256 && cout2 == 64;
+  return limbs == 3 && cin == 64 && cout1 == 256 && (cout2 == 64 || cout2 == 0);
 }
 
-int launch_resident_pair(const ConvArgs& a, const ConvArgs& b, int limbs, hipStream_t s) {
-  if (!resident_pair_supported(a.cin, a.cout, b.cout, limbs) || a.kh != 1 || a.kw != 1 || a.stride != 1 ||
-      a.pad != 0 || b.kh != 1 || b.kw != 1 || b.stride != 1 || b.pad != 0 || b.cin != a.cout || b.M != a.M)
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_pair_fwd: shapes not built (64->256->64 1x1, stride 1, 3 "
-                                "activation limbs, the second conv on the first one's output)");
-  if (!a.yq || !b.yq || a.y || b.y || a.residual || !a.res_q || b.res_q || b.residual || a.y_absmax ||
-      b.y_absmax || a.has_offset || b.has_offset || !a.relu || !b.relu || a.overflow != b.overflow)
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_pair_fwd: static-range limb-plane outputs, ReLU, a limb-plane "
-                                "residual on the first conv only, exact weight codes, one overflow flag");
-  return launch_pair_one<3, 1, 4, 1>(a, b, s);
+int launch_resident_chain(const ConvArgs& a, const ConvArgs* b, const ConvArgs* d, int limbs, hipStream_t s) {
+  auto conv1x1 = [](const ConvArgs& c) { return c.kh == 1 && c.kw == 1 && c.stride == 1 && c.pad == 0 && !c.s2d; };
+  if (!resident_pair_supported(a.cin, a.cout, b ? b->cout : 0, limbs) || !conv1x1(a) ||
+      (b && (!conv1x1(*b) || b->cin != a.cout || b->M != a.M)) ||
+      (d && (!conv1x1(*d) || d->cin != a.cin || d->cout != a.cout || d->h != a.h || d->w != a.w || d->n != a.n)))
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_chain_fwd: shapes not built (conv3 64->256 1x1 stride 1, 3 activation "
+                                "limbs; the next conv1 256->64 on its output; a downsample 64->256 1x1 stride 1 on "
+                                "the same pixels)");
+  if (!a.yq || a.y || a.residual || a.y_absmax || !a.relu || (!a.res_q) == (d == nullptr) ||
+      (b && (!b->yq || b->y || b->residual || b->res_q || b->y_absmax || b->has_offset || !b->relu ||
+             b->overflow != a.overflow)) ||
+      (d && (!d->yq_inv || d->y || d->residual || d->res_q || d->has_offset || d->relu || d->overflow != a.overflow)))
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_chain_fwd: static-range limb-plane outputs, ReLU, the identity as "
+                                "limb planes or as the fused downsample (exactly one), one overflow flag");
+  const ConvArgs& bb = b ? *b : a;
+  const ConvArgs& dd = d ? *d : a;
+  const bool off = a.has_offset != 0;
+  if (d) {
+    // conv3 + the fused downsample: 128-channel slabs (three workgroups per CU). With the chained
+    // conv1 as well it needs one 256-channel slab, ~410 registers per lane and one workgroup per
+    // CU: measured 4-5 % slower on the R50 step than without (profiles/r06_chain_fused_ds.txt); not built
+    if (b) return fail(SMPQ_E_INVALID, "smpq_conv2d_chain_fwd: the fused downsample is built without a chained conv1");
+    return off ? launch_chain_one<3, 1, 2, 0, true, 3>(a, bb, dd, s) : launch_chain_one<3, 1, 2, 0, false, 3>(a, bb, dd, s);
+  }
+  if (!b) return fail(SMPQ_E_INVALID, "smpq_conv2d_chain_fwd: nothing to chain (plain conv3: smpq_conv2d_fwd_q)");
+  return off ? launch_chain_one<3, 1, 4, 1, true, 0>(a, bb, dd, s) : launch_chain_one<3, 1, 4, 1, false, 0>(a, bb, dd, s);
 }
 
 }  // namespace smpq

@@ -55,6 +55,10 @@ _PROTOS = {
                                   _vp, _i, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, ctypes.c_float, _i, _vp]),
     "smpq_weights_kmajor": (_i, [_vp, _i, _i, _i, _vp, _vp]),
     "smpq_conv2d_pair_supported": (_i, [_i] * 4),
+    "smpq_conv2d_chain_supported": (_i, [_i] * 4),
+    "smpq_conv2d_chain_fwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, ctypes.c_float,
+                                   _vp, _vp, _vp, _i, _vp, _vp, ctypes.c_float, _vp, ctypes.c_float, _vp,
+                                   _vp, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _vp]),
     "smpq_conv2d_pair_fwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, ctypes.c_float, _vp,
                                   ctypes.c_float, _vp, _vp, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _vp]),
     "smpq_maxpool_limbs": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp]),

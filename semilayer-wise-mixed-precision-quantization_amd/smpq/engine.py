@@ -73,6 +73,9 @@ STREAMS = [int(_os.environ.get("SMPQ_STREAMS", "2"))]
 # static range: a Bottleneck's conv3 and the next block's conv1 as ONE launch where the pair kernel
 # is built (ops.conv_pair_q: conv1 reads conv3's output tile from LDS; bitwise the two launches)
 PAIR_1X1 = [_os.environ.get("SMPQ_PAIR_1X1", "1") != "0"]
+# static range: a stage's first Bottleneck computes its 1x1 / stride-1 downsample inside conv3's
+# tiles (ops.conv_chain_q; its output limb planes are never written) where that is built
+FUSE_DS = [_os.environ.get("SMPQ_FUSE_DS", "1") != "0"]
 stats.setdefault("graph_captures", 0)
 stats.setdefault("graph_replays", 0)
 
@@ -257,36 +260,56 @@ def _side_stream(device, lane):
     return _stream((device, "ds", lane))
 
 
-def _pair_plan(blk, nxt, ctx, identity):
-    """(conv3 plan, next conv1 plan) when blk.conv3 and nxt.conv1 can run as one pair launch
-    (static ranges, exact codes, 1x1 / stride 1 / pad 0 both, a limb-plane identity, a built
-    shape), else None."""
+def _1x1(c):
+    return c.kernel_size == (1, 1) and c.stride == (1, 1) and c.padding == (0, 0) and c.groups == 1
+
+
+def _exact(plan):
+    return plan is not None and (plan[0].dim() == 2 or plan[0].shape[0] == 1)
+
+
+def _pair_plan(blk, nxt, ctx):
+    """The next block's conv1 plan when it can be chained onto blk.conv3 (static ranges, exact
+    codes without offsets, 1x1 / stride 1 / pad 0 both, a built shape), else None."""
     if not (PAIR_1X1[0] and nxt is not None and ctx is not None and ctx.ranges is not None
-            and hasattr(blk, "conv3") and hasattr(nxt, "conv3") and nxt.downsample is None
-            and isinstance(identity, Act) and identity.f32 is None and identity.q is not None
-            and identity.rng is not None):
+            and hasattr(blk, "conv3") and hasattr(nxt, "conv3") and nxt.downsample is None):
         return None
     c3, c1 = blk.conv3, nxt.conv1
-    if id(c3) not in ctx.ranges or id(c1) not in ctx.ranges:
+    if id(c3) not in ctx.ranges or id(c1) not in ctx.ranges or not (_1x1(c3) and _1x1(c1)):
         return None
-    for c in (c3, c1):
-        if c.kernel_size != (1, 1) or c.stride != (1, 1) or c.padding != (0, 0) or c.groups != 1:
-            return None
     p3, p1 = conv_plan(c3, blk.bn3), conv_plan(c1, nxt.bn1)
-    if p3 is None or p1 is None:
+    if not (_exact(p3) and _exact(p1)) or p1[1] is not None:
         return None
-    for codes, offset in ((p3[0], p3[1]), (p1[0], p1[1])):
-        if offset is not None or not (codes.dim() == 2 or codes.shape[0] == 1):
-            return None
-    if identity.q.shape[0] != 3 or not ops.conv_pair_supported(c3.in_channels, c3.out_channels, c1.out_channels):
+    if not ops.conv_chain_supported(c3.in_channels, c3.out_channels, c1.out_channels):
         return None
-    return p3, p1
+    return p1
+
+
+def _ds_fuse_plan(blk, x, ctx):
+    """The downsample's plan when it can run inside blk.conv3's tiles (ops.conv_chain_q): a
+    Bottleneck whose conv1 / conv2 keep the resolution, a 1x1 / stride-1 downsample conv + BN over
+    conv3's K and output channels in 24-bit fixed point, static ranges for both, a built shape."""
+    if not (FUSE_DS[0] and ctx is not None and ctx.ranges is not None and hasattr(blk, "conv3")
+            and isinstance(blk.downsample, torch.nn.Sequential) and len(blk.downsample) == 2
+            and x.q is not None and x.amax is not None and x.q.shape[0] == 3):
+        return None
+    dc, dbn, c3 = blk.downsample[0], blk.downsample[1], blk.conv3
+    if not (isinstance(dbn, torch.nn.BatchNorm2d) and _1x1(dc) and _1x1(c3) and blk.conv1.stride == (1, 1)
+            and blk.conv2.stride == (1, 1) and dc.in_channels == c3.in_channels
+            and dc.out_channels == c3.out_channels and id(dc) in ctx.ranges and id(c3) in ctx.ranges):
+        return None
+    pd, p3 = conv_plan(dc, dbn), conv_plan(c3, blk.bn3)
+    if pd is None or not _exact(p3) or pd[1] is not None or pd[0].dim() != 3 or pd[0].shape[0] != 3:
+        return None
+    if not ops.conv_chain_supported(c3.in_channels, c3.out_channels, 0):
+        return None
+    return pd
 
 
 def block_forward(blk, x, ctx=None, last=False, t1=None, nxt=None):
     """One BasicBlock / Bottleneck on an Act; returns (output Act, the next block's conv1 output
     Act or None). ``t1``: this block's conv1 output when the previous block already computed it
-    (pair launch); ``nxt``: the next block, whose conv1 is chained onto this block's conv3 when
+    (chain launch); ``nxt``: the next block, whose conv1 is chained onto this block's conv3 when
     _pair_plan allows. In static mode no
     activation is stored in fp32 except the downsample's identity and the last block's output
     (avgpool): the identity of a block without downsample is read from its input's limb planes.
@@ -294,12 +317,26 @@ def block_forward(blk, x, ctx=None, last=False, t1=None, nxt=None):
     Static mode: the downsample branch (resnet.py:188-192) depends only on the block input, so it
     runs beside conv1: outside batch slices on a side stream that joins before the conv that adds
     it (fork/join inside the captured graph); a single launch holding both convs was measured
-    slower than the two launches (profiles/r03_pair_bench.txt). Every conv computes exactly what
-    it computes serially, so the result is bitwise the same (tests/test_gpu.py)."""
+    slower than the two launches (profiles/r03_pair_bench.txt). Where _ds_fuse_plan allows, it
+    runs inside conv3's own tiles instead (ops.conv_chain_q) and its output is never written. Every
+    conv computes exactly what it computes serially, so the result is bitwise the same
+    (tests/test_gpu.py, tests/test_gpu_pair.py)."""
     side = None
+    dsplan = None if last else _ds_fuse_plan(blk, x, ctx)
+
+    def downsample():
+        return run_conv(blk.downsample[0], blk.downsample[1], x, relu=False, ctx=ctx, want_f32=False)
+
+    def as_identity(ds):
+        # static mode: the identity as calibrated-range limb planes (3 B/element instead of fp32)
+        return ds if (ds.f32 is None and ds.q is not None and ds.rng is not None) else ds.f32
+
     # (not inside a batch slice: a fork nested in a slice's fork crashes hipStreamEndCapture on
     # ROCm 7.2 / torch 2.10 — reproduced with torch alone by tools/repro_nested_fork.py)
-    if blk.downsample is not None and CONCURRENT_DS[0] and ctx is not None and ctx.ranges is not None \
+    identity = None
+    if dsplan is not None:
+        pass  # computed in conv3's tiles
+    elif blk.downsample is not None and CONCURRENT_DS[0] and ctx is not None and ctx.ranges is not None \
             and ctx.lane is None and x.q is not None:  # both branches read the input's limb planes
         main = torch.cuda.current_stream()
         side = _side_stream(x.q.device, ctx.lane)
@@ -308,12 +345,9 @@ def block_forward(blk, x, ctx=None, last=False, t1=None, nxt=None):
             # allocated on the side stream, consumed on main after the join; freed blocks are
             # reused by the side stream only after its next wait on main (the next fork), which
             # is ordered after every consumer, so no record_stream is needed (none in a capture)
-            ds = run_conv(blk.downsample[0], blk.downsample[1], x, relu=False, ctx=ctx, want_f32=False)
+            identity = as_identity(downsample())
     elif blk.downsample is not None:
-        ds = run_conv(blk.downsample[0], blk.downsample[1], x, relu=False, ctx=ctx, want_f32=False)
-    if blk.downsample is not None:
-        # static mode: the identity as calibrated-range limb planes (3 B/element instead of fp32)
-        identity = ds if (ds.f32 is None and ds.q is not None and ds.rng is not None) else ds.f32
+        identity = as_identity(downsample())
     elif x.f32 is not None or x.q is None or x.rng is None:
         identity = x.f32
     else:
@@ -329,19 +363,41 @@ def block_forward(blk, x, ctx=None, last=False, t1=None, nxt=None):
     if hasattr(blk, "conv3"):  # Bottleneck (resnet.py:97-116)
         t2 = run_conv(blk.conv2, blk.bn2, t1, True, ctx=ctx, want_f32=False)
         join()
-        pair = None if last else _pair_plan(blk, nxt, ctx, identity)
-        if pair is not None and t2.q is not None and t2.amax is not None:
-            # conv3 (+ identity, ReLU) and the next block's conv1 (ReLU) in one launch
-            (codes3, _, cs3, sh3, kind3), (codes1, _, cs1, sh1, kind1) = pair
-            c3, c1 = blk.conv3, nxt.conv1
-            rng3, rng1 = ctx.ranges[id(c3)], ctx.ranges[id(c1)]
-            am3 = ctx.range_tensor(c3)
-            yq3, yq1 = ops.conv_pair_q(t2.q, t2.amax, codes3, cs3, sh3, identity.q, identity.rng, rng3, am3,
-                                       codes1, cs1, sh1, rng1, ctx.overflow)
-            stats["hip_conv"] += 2
-            stats["pair_conv"] = stats.get("pair_conv", 0) + 1
-            c3.last_path, c1.last_path = "hip-%s-pair" % kind3, "hip-%s-pair" % kind1
-            return Act(q=yq3, amax=am3, rng=rng3), Act(q=yq1, amax=ctx.range_tensor(c1), rng=rng1)
+        # (a fused downsample runs without a chained conv1: smpq_conv2d_chain_fwd)
+        p1 = None if (last or dsplan is not None) else _pair_plan(blk, nxt, ctx)
+        ident_q = dsplan is not None or (isinstance(identity, Act) and identity.f32 is None
+                                         and identity.q is not None and identity.rng is not None)
+        chain = (dsplan is not None or p1 is not None) and ident_q and t2.q is not None and t2.amax is not None \
+            and t2.q.shape[0] == 3 and (dsplan is None or t2.q.shape[1:4] == x.q.shape[1:4])
+        if dsplan is not None and not chain:
+            identity = as_identity(downsample())  # (not expected: conv2 ran outside the static path)
+        if chain:
+            # conv3 (+ identity, ReLU) with its downsample and / or the next block's conv1, one launch
+            c3 = blk.conv3
+            codes3, off3, cs3, sh3, kind3 = conv_plan(c3, blk.bn3)
+            rng3, am3 = ctx.ranges[id(c3)], ctx.range_tensor(c3)
+            dsarg = nxtarg = None
+            if dsplan is not None:
+                dcodes, _, dcs, dsh, dkind = dsplan
+                dsarg = (x.q, x.amax, dcodes, dcs, dsh, ctx.ranges[id(blk.downsample[0])])
+            if p1 is not None:
+                nxtarg = (p1[0], p1[2], p1[3], ctx.ranges[id(nxt.conv1)])
+            yq3, yq1 = ops.conv_chain_q(t2.q, t2.amax, codes3, off3, cs3, sh3, rng3, am3, ctx.overflow,
+                                        residual_q=None if dsarg else identity.q,
+                                        residual_range=None if dsarg else identity.rng, ds=dsarg, nxt=nxtarg)
+            stats["hip_conv"] += 1 + (dsarg is not None) + (nxtarg is not None)
+            stats["fixed_conv"] += dsarg is not None
+            stats["chain_conv"] = stats.get("chain_conv", 0) + 1
+            stats["pair_conv"] = stats.get("pair_conv", 0) + (nxtarg is not None)
+            stats["fused_ds"] = stats.get("fused_ds", 0) + (dsarg is not None)
+            c3.last_path = "hip-%s-chain" % kind3
+            if dsarg is not None:
+                blk.downsample[0].last_path = "hip-%s-chain" % dkind
+            nt1 = None
+            if nxtarg is not None:
+                nxt.conv1.last_path = "hip-%s-chain" % p1[4]
+                nt1 = Act(q=yq1, amax=ctx.range_tensor(nxt.conv1), rng=nxtarg[3])
+            return Act(q=yq3, amax=am3, rng=rng3), nt1
         return run_conv(blk.conv3, blk.bn3, t2, True, residual=identity, ctx=ctx, want_amax=out_amax,
                         want_f32=last), None
     # BasicBlock (resnet.py:55-68)
@@ -666,7 +722,7 @@ def _graph_base(cal):
     """What every captured graph of a model depends on besides its input's shape and address:
     the calibration (ranges, signature) and the forward's structure knobs."""
     return (cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0], CONCURRENT_DS[0], STREAMS[0],
-            ops.KMAJOR[0], PAIR_1X1[0])
+            ops.KMAJOR[0], PAIR_1X1[0], FUSE_DS[0])
 
 
 def _graph_key(model, x, cal):

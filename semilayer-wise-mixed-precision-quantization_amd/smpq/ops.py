@@ -506,11 +506,116 @@ def conv_pair_supported(cin, cout1, cout2, limbs=3):
     return bool(_lib.load().smpq_conv2d_pair_supported(int(cin), int(cout1), int(cout2), int(limbs)))
 
 
+def conv_chain_supported(cin, cout1, cout2=0, limbs=3):
+    """Does smpq_conv2d_chain_fwd run a conv3 cin -> cout1 (+ a fused downsample) (-> next conv1
+    cout1 -> cout2; 0: none)?"""
+    return bool(_lib.load().smpq_conv2d_chain_supported(int(cin), int(cout1), int(cout2), int(limbs)))
+
+
+def _one_limb(codes, what):
+    _req(codes.dim() == 2 or codes.shape[0] == 1, "chain: %s needs exact codes (one weight limb)" % what)
+    return codes[0] if codes.dim() == 3 else codes
+
+
+def conv_chain_q(xq, x_absmax, codes1, offset1, col_scale1, col_shift1, emit_range1, y1_absmax, overflow,
+                 residual_q=None, residual_range=None, ds=None, nxt=None):
+    """A Bottleneck's conv3 (1x1 + folded BN + identity + ReLU, exact codes, optional weight offsets)
+    in one launch with (csrc/conv_resident.hip, smpq_conv2d_chain_fwd):
+      - its identity: ``residual_q`` limb planes (+ ``residual_range``), or ``ds`` = (ds_xq,
+        ds_x_absmax, ds_codes [3, cout1, cin], ds_col_scale, ds_col_shift, ds_range): the block's 1x1
+        stride-1 downsample computed in the same tiles (its output codes feed the residual; never
+        written);
+      - ``nxt`` = (codes2, col_scale2, col_shift2, emit_range2): the next block's conv1 (ReLU) on
+        conv3's output tile.
+    Returns (yq1, yq2 or None), bitwise what the separate launches write; ``overflow`` covers every
+    output of the chain (the downsample's included)."""
+    _req(xq.is_cuda and xq.dtype == torch.int8 and xq.dim() == 5 and xq.is_contiguous(), "chain: xq")
+    limbs, n, h, w, cin = xq.shape
+    c1 = _one_limb(codes1, "conv3")
+    cout1 = c1.shape[0]
+    c2 = _one_limb(nxt[0], "conv1") if nxt is not None else None
+    cout2 = c2.shape[0] if c2 is not None else 0
+    _req(c1.shape == (cout1, cin) and c1.is_contiguous() and c1.dtype == torch.int8, "chain: conv3 codes")
+    _req(c2 is None or (c2.shape == (cout2, cout1) and c2.is_contiguous() and c2.dtype == torch.int8),
+         "chain: conv1 codes")
+    _req(conv_chain_supported(cin, cout1, cout2, limbs), "chain: shape not built")
+    _req((residual_q is None) != (ds is None), "chain: one identity source (residual_q or ds)")
+    _req(offset1 is None or (offset1.dtype == torch.int32 and offset1.numel() == cout1), "chain: offset")
+    if residual_q is not None:
+        _req(residual_q.shape == (limbs, n, h, w, cout1) and residual_q.dtype == torch.int8
+             and residual_q.is_contiguous() and residual_range is not None and residual_range > 0, "chain: residual_q")
+    vecs = [(col_scale1, cout1), (col_shift1, cout1)]
+    if ds is not None:
+        dxq, dam, dcodes, dcs, dsh, drng = ds
+        _req(dxq.shape == xq.shape and dxq.dtype == torch.int8 and dxq.is_contiguous() and dam.numel() == n,
+             "chain: downsample input")
+        _req(dcodes.shape == (3, cout1, cin) and dcodes.dtype == torch.int8 and dcodes.is_contiguous(),
+             "chain: downsample codes [3, cout, cin]")
+        _req(drng > 0, "chain: downsample range")
+        vecs += [(dcs, cout1), (dsh, cout1)]
+    if nxt is not None:
+        vecs += [(nxt[1], cout2), (nxt[2], cout2)]
+        _req(y1_absmax is not None and y1_absmax.numel() == n, "chain: y1_absmax")
+    for t, c in vecs:
+        _req(t.dtype == torch.float32 and t.numel() == c and t.is_contiguous() and t.device == xq.device,
+             "chain: col vectors")
+    _req(x_absmax.numel() == n and overflow is not None and overflow.dtype == torch.int32
+         and overflow.device == xq.device, "chain: absmax / overflow")
+    nchunk = PLANE_LIMIT // (limbs * h * w * max(cin, cout1))
+    _req(nchunk >= 1, "chain: one image's planes exceed 2 GiB")
+    if n > nchunk:  # 32-bit buffer offsets: image chunks (independent images, the same result)
+        yq1 = torch.empty(limbs, n, h, w, cout1, dtype=torch.int8, device=xq.device)
+        yq2 = torch.empty(limbs, n, h, w, cout2, dtype=torch.int8, device=xq.device) if nxt is not None else None
+        for i0 in range(0, n, nchunk):
+            i1 = min(n, i0 + nchunk)
+            a, b = conv_chain_q(
+                xq[:, i0:i1].contiguous(), x_absmax[i0:i1], codes1, offset1, col_scale1, col_shift1, emit_range1,
+                None if y1_absmax is None else y1_absmax[i0:i1], overflow,
+                residual_q=None if residual_q is None else residual_q[:, i0:i1].contiguous(),
+                residual_range=residual_range,
+                ds=None if ds is None else (ds[0][:, i0:i1].contiguous(), ds[1][i0:i1]) + tuple(ds[2:]), nxt=nxt)
+            yq1[:, i0:i1].copy_(a)
+            if b is not None:
+                yq2[:, i0:i1].copy_(b)
+        return yq1, yq2
+    yq1 = torch.empty(limbs, n, h, w, cout1, dtype=torch.int8, device=xq.device)
+    yq2 = torch.empty(limbs, n, h, w, cout2, dtype=torch.int8, device=xq.device) if nxt is not None else None
+    lib = _lib.load()
+    hook = _CONV_HOOK[0]
+    if hook is not None:
+        hook.begin()
+    P = _lib.ptr
+    with torch.cuda.device(xq.device):
+        _lib.check(lib.smpq_conv2d_chain_fwd(
+            P(xq), P(x_absmax), n, h, w, cin, P(c1), P(offset1), cout1, P(col_scale1), P(col_shift1),
+            P(residual_q), float(residual_range or 0.0),
+            P(ds[0]) if ds else None, P(ds[1]) if ds else None, P(ds[2]) if ds else None, 3 if ds else 0,
+            P(ds[3]) if ds else None, P(ds[4]) if ds else None, float(ds[5]) if ds else 0.0,
+            P(yq1), float(emit_range1), P(y1_absmax),
+            P(c2), cout2, P(nxt[1]) if nxt else None, P(nxt[2]) if nxt else None, P(yq2),
+            float(nxt[3]) if nxt else 0.0, P(overflow), _lib.stream_ptr()), "smpq_conv2d_chain_fwd")
+    if hook is not None:
+        # one launch doing every chained conv's work; the reads / writes it removes are not counted
+        w1 = alg_work(n, h, w, cin, cout1, 1, 1, h, w, limbs, 1, False, True, False, residual_q is not None)
+        ops_, nbytes, shape = w1["ops"], w1["bytes"], "%4d->%4d" % (cin, cout1)
+        if ds is not None:
+            wd = alg_work(n, h, w, cin, cout1, 1, 1, h, w, limbs, 3, False, False, False, False)
+            ops_ += wd["ops"]
+            nbytes += wd["bytes"]  # the downsample's input and weights (its output never leaves the CU)
+            shape += "+ds"
+        if nxt is not None:
+            w2 = alg_work(n, h, w, cout1, cout2, 1, 1, h, w, limbs, 1, False, True, False, False)
+            ops_ += w2["ops"]
+            nbytes += w2["bytes"] - limbs * n * h * w * cout1  # conv1 reads conv3's tile from LDS
+            shape += "->%4d" % cout2
+        hook.end({"ops": ops_, "bytes": nbytes, "passes": w1["passes"], "shape": "%s k1 %3d chain" % (shape, h)})
+    return yq1, yq2
+
+
 def conv_pair_q(xq, x_absmax, codes1, col_scale1, col_shift1, residual_q, residual_range, emit_range1,
                 y1_absmax, codes2, col_scale2, col_shift2, emit_range2, overflow):
     """A Bottleneck's conv3 (1x1 + folded BN + limb-plane identity + ReLU) chained with the next
-    block's conv1 (1x1 + folded BN + ReLU) in one launch (csrc/conv_resident.hip, the pair path):
-    returns (yq1, yq2), bitwise
+    block's conv1 (1x1 + folded BN + ReLU) in one launch: returns (yq1, yq2), bitwise
 
         _, yq1 = conv2d_q(xq, x_absmax, codes1, None, 1, 1, 1, 0, col_scale1, col_shift1, relu=True,
                           emit_range=emit_range1, overflow=overflow, want_f32=False,
@@ -518,56 +623,12 @@ def conv_pair_q(xq, x_absmax, codes1, col_scale1, col_shift1, residual_q, residu
         _, yq2 = conv2d_q(yq1, y1_absmax, codes2, None, 1, 1, 1, 0, col_scale2, col_shift2, relu=True,
                           emit_range=emit_range2, overflow=overflow, want_f32=False)
 
-    without reading yq1 back from HBM. Exact weight codes only (one limb, no offsets)."""
-    _req(xq.is_cuda and xq.dtype == torch.int8 and xq.dim() == 5 and xq.is_contiguous(), "pair: xq")
-    limbs, n, h, w, cin = xq.shape
-    c1 = codes1[0] if codes1.dim() == 3 else codes1
-    c2 = codes2[0] if codes2.dim() == 3 else codes2
-    _req(codes1.dim() == 2 or codes1.shape[0] == 1, "pair: conv3 needs exact codes (one weight limb)")
-    _req(codes2.dim() == 2 or codes2.shape[0] == 1, "pair: conv1 needs exact codes (one weight limb)")
-    cout1, cout2 = c1.shape[0], c2.shape[0]
-    _req(c1.shape == (cout1, cin) and c2.shape == (cout2, cout1) and c1.is_contiguous() and c2.is_contiguous()
-         and c1.dtype == torch.int8 and c2.dtype == torch.int8, "pair: codes shapes")
-    _req(conv_pair_supported(cin, cout1, cout2, limbs), "pair: shape not built")
-    _req(residual_q.shape == (limbs, n, h, w, cout1) and residual_q.dtype == torch.int8
-         and residual_q.is_contiguous(), "pair: residual_q")
-    _req(x_absmax.numel() == n and y1_absmax.numel() == n, "pair: absmax")
-    for t, c in ((col_scale1, cout1), (col_shift1, cout1), (col_scale2, cout2), (col_shift2, cout2)):
-        _req(t.dtype == torch.float32 and t.numel() == c and t.is_contiguous() and t.device == xq.device,
-             "pair: col vectors")
-    _req(overflow is not None and overflow.dtype == torch.int32 and overflow.device == xq.device, "pair: overflow")
-    nchunk = PLANE_LIMIT // (limbs * h * w * max(cin, cout1))
-    _req(nchunk >= 1, "pair: one image's planes exceed 2 GiB")
-    if n > nchunk:  # 32-bit buffer offsets: image chunks (independent images, the same result)
-        yq1 = torch.empty(limbs, n, h, w, cout1, dtype=torch.int8, device=xq.device)
-        yq2 = torch.empty(limbs, n, h, w, cout2, dtype=torch.int8, device=xq.device)
-        for i0 in range(0, n, nchunk):
-            i1 = min(n, i0 + nchunk)
-            a, b = conv_pair_q(xq[:, i0:i1].contiguous(), x_absmax[i0:i1], codes1, col_scale1, col_shift1,
-                               residual_q[:, i0:i1].contiguous(), residual_range, emit_range1, y1_absmax[i0:i1],
-                               codes2, col_scale2, col_shift2, emit_range2, overflow)
-            yq1[:, i0:i1].copy_(a)
-            yq2[:, i0:i1].copy_(b)
-        return yq1, yq2
-    yq1 = torch.empty(limbs, n, h, w, cout1, dtype=torch.int8, device=xq.device)
-    yq2 = torch.empty(limbs, n, h, w, cout2, dtype=torch.int8, device=xq.device)
-    lib = _lib.load()
-    hook = _CONV_HOOK[0]
-    if hook is not None:
-        hook.begin()
-    with torch.cuda.device(xq.device):
-        _lib.check(lib.smpq_conv2d_pair_fwd(
-            _lib.ptr(xq), _lib.ptr(x_absmax), n, h, w, cin, _lib.ptr(c1), cout1, _lib.ptr(col_scale1),
-            _lib.ptr(col_shift1), _lib.ptr(residual_q), float(residual_range), _lib.ptr(yq1), float(emit_range1),
-            _lib.ptr(y1_absmax), _lib.ptr(c2), cout2, _lib.ptr(col_scale2), _lib.ptr(col_shift2), _lib.ptr(yq2),
-            float(emit_range2), _lib.ptr(overflow), _lib.stream_ptr()), "smpq_conv2d_pair_fwd")
-    if hook is not None:
-        # one launch doing both convs' work; the second conv's activation read is gone
-        w1 = alg_work(n, h, w, cin, cout1, 1, 1, h, w, limbs, 1, False, True, False, True)
-        w2 = alg_work(n, h, w, cout1, cout2, 1, 1, h, w, limbs, 1, False, True, False, False)
-        hook.end({"ops": w1["ops"] + w2["ops"], "bytes": w1["bytes"] + w2["bytes"] - limbs * n * h * w * cout1,
-                  "passes": w1["passes"], "shape": "%4d->%4d->%4d k1 %3d pair" % (cin, cout1, cout2, h)})
-    return yq1, yq2
+    without reading yq1 back from HBM (conv_chain_q with the next conv and no downsample)."""
+    c1, c2 = _one_limb(codes1, "conv3"), _one_limb(codes2, "conv1")
+    _req(conv_pair_supported(xq.shape[-1], c1.shape[0], c2.shape[0], xq.shape[0]), "pair: shape not built")
+    return conv_chain_q(xq, x_absmax, codes1, None, col_scale1, col_shift1, emit_range1, y1_absmax, overflow,
+                        residual_q=residual_q, residual_range=residual_range,
+                        nxt=(codes2, col_scale2, col_shift2, emit_range2))
 
 
 # ---- per-shape tile choice (cf. cudnn.benchmark=True, resnet50_main.py:10) ---------------------
@@ -713,11 +774,13 @@ def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, 
     # now): the key does not carry relu / y_absmax, so other calls of a key never see them
     halo_ok = bool(relu and emit_range is not None and not want_f32 and residual is None and residual_q is None
                    and y_absmax is None and out is None and kh == 3 and kw == 3 and stride == 1 and pad == 1)
-    # the weight-stationary 1x1 tiles: the static-range limb-plane epilogue without weight offsets,
-    # built for the downsamples (3 weight limbs, no ReLU or residual) and for exact-code convs with
-    # ReLU + a limb-plane residual, ReLU only, or neither (smpq_conv2d_tile_supported checks the shape)
+    # the weight-stationary 1x1 tiles: the static-range limb-plane epilogue, built for the
+    # downsamples (3 weight limbs, no ReLU or residual) and for exact-code convs with ReLU + a
+    # limb-plane residual, ReLU only (both also with weight offsets), or neither
+    # (smpq_conv2d_tile_supported checks the shape)
     res_ok = bool(emit_range is not None and not want_f32 and residual is None and y_absmax is None
-                  and out is None and offset is None and kh == 1 and kw == 1 and pad == 0
+                  and out is None and kh == 1 and kw == 1 and pad == 0
+                  and (offset is None or (wlimbs == 1 and relu))
                   and (not (relu or residual_q is not None) if wlimbs == 3 else (relu or residual_q is None)))
     cands = [c for c in tile_configs() if _tile_fits(c, limbs, wlimbs, cout, cin, kh)
              and (halo_ok or tile_kind(c) != TILE_HALO3X3) and (res_ok or tile_kind(c) != TILE_RESIDENT1X1)]

@@ -1,8 +1,8 @@
 """Weight-stationary 1x1 tiles (csrc/conv_resident.hip, tile kind TILE_RESIDENT1X1): their
 static-range limb-plane outputs and overflow flags equal the LDS-DMA kernel's bit for bit — 24-bit
 fixed-point (3-limb) weights as in the downsample convs and exact codes (1 limb), with and without
-ReLU, with a limb-plane residual, stride 1 and 2, K 64 .. 1024, partial last tiles, several tiles
-per workgroup, in range and overflowing —
+ReLU, with a limb-plane residual, with weight offsets, stride 1 and 2, K 64 .. 1024, partial last
+tiles, several tiles per workgroup, in range and overflowing —
 and the calls they do not run are refused before launching. Every call goes through the C-ABI."""
 import pytest
 import torch
@@ -108,6 +108,39 @@ def test_resident_residual_equals_lds_dma(gpu, cin, cout, n, h):
                 assert torch.equal(ovf, ovf0), (c, rr, frac)
 
 
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("cin,cout,n,h", [(64, 256, 2, 28), (256, 64, 2, 21), (256, 1024, 1, 14), (1024, 256, 2, 7)])
+def test_resident_weight_offsets_equal_lds_dma(gpu, cin, cout, n, h, res):
+    """Exact codes off-centre (per-channel weight offsets, ReLU; with and without the residual):
+    the v_dot4 digit-sum correction gives the LDS-DMA kernel's limb planes bit for bit."""
+    from smpq import ops
+    cfgs = [c for c in _res_cfgs(ops) if ops._tile_fits(c, 3, 1, cout, cin, 1)]
+    assert cfgs
+    codes, _, scale = _layer(gpu, 1, 11 * n + h + cin, cin, cout)
+    g = torch.Generator().manual_seed(n + 13 * h)
+    off = torch.randint(-100, 100, (cout,), generator=g, dtype=torch.int32).to(gpu)
+    x = torch.relu(torch.randn(n, h, h, cin, generator=g)).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, 3)
+    shift = torch.linspace(-0.5, 0.5, cout, device=gpu)
+    kw = {}
+    if res:
+        r = torch.relu(torch.randn(n, h, h, cout, generator=g)).to(gpu)
+        kw = dict(residual_q=ops.act_quantize(r, torch.full((n,), 5.0, device=gpu), 3), residual_range=5.0)
+    ref = ops.conv2d_q(xq, am, codes, off, 1, 1, 1, 0, scale, shift, relu=True, **kw)
+    for frac in (2.0, 0.4):
+        rng = float(ref.abs().max()) * frac
+        ovf0 = torch.zeros(1, dtype=torch.int32, device=gpu)
+        _, yq0 = ops.conv2d_q(xq, am, codes, off, 1, 1, 1, 0, scale, shift, relu=True, tile_cfg=-1, emit_range=rng,
+                              overflow=ovf0, want_f32=False, **kw)
+        for c in cfgs:
+            ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+            _, yq = ops.conv2d_q(xq, am, codes, off, 1, 1, 1, 0, scale, shift, relu=True, tile_cfg=c, emit_range=rng,
+                                 overflow=ovf, want_f32=False, **kw)
+            assert torch.equal(yq, yq0), (c, frac)
+            assert torch.equal(ovf, ovf0), (c, frac)
+
+
 def test_resident_many_tiles_per_workgroup(gpu):
     """More tiles than resident workgroups (each walks ~25 tiles), the R50 downsample's shape at a
     quarter of the batch: bitwise the LDS-DMA kernel's limb planes."""
@@ -159,6 +192,6 @@ def test_resident_refuses_what_it_does_not_run(gpu):
                      want_f32=False)
     off = torch.zeros(256, dtype=torch.int32, device=gpu)
     off[3] = 5
-    with pytest.raises(_lib.SmpqError, match="resident"):  # weight offsets
+    with pytest.raises(_lib.SmpqError, match="resident"):  # weight offsets without ReLU
         ops.conv2d_q(xq, am, codes, off, 1, 1, 1, 0, scale, shift, tile_cfg=c, emit_range=1.0, overflow=ovf,
                      want_f32=False)

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Time the chained Bottleneck pair (ops.conv_pair_q: conv3 + identity + ReLU -> next conv1 + ReLU,
-one launch) against the two launches it replaces (each on its table / autotuned tile), at the R50
-layer1 / layer2 shapes; checks bitwise equality. Diagnostics only.
+"""Time the chained Bottleneck tails against the launches they replace (each on its table /
+autotuned tile), at the R50 layer1 shapes, and check bitwise equality: the pair (ops.conv_pair_q:
+conv3 + identity + ReLU -> next conv1 + ReLU) and conv3 with its fused downsample
+(ops.conv_chain_q ds=...). Diagnostics only.
 
     TB_BATCH=128 python tools/pair_bench.py"""
 import os
@@ -35,7 +36,7 @@ def timed(fn, reps=20):
     return ev[0].elapsed_time(ev[1]) / reps * 1e3
 
 
-for cin, c1, c2, h in ((64, 256, 64, 56), (128, 512, 128, 28)):
+for cin, c1, c2, h in ((64, 256, 64, 56),):
     g = torch.Generator(device=dev).manual_seed(0)
 
     def codes(co, ci):
@@ -76,3 +77,30 @@ for cin, c1, c2, h in ((64, 256, 64, 56), (128, 512, 128, 28)):
     print("B=%d %4d->%4d->%4d @%d: two launches %.1f us (conv3 alone %.1f, conv1 alone %.1f), pair %.1f us (%.2fx)%s"
           % (B, cin, c1, c2, h, t_two, t_first, t_second, t_pair, t_two / t_pair, "" if same else "  MISMATCH"),
           flush=True)
+
+    # conv3 + the fused downsample vs the downsample launch + conv3 with the limb-plane identity
+    wds = torch.randn(c1, cin, 1, 1, device=dev, generator=g) * 0.05
+    dcodes, _, dscale, _ = ops.pack_weights_ex(wds, None, 3)
+    dsh = torch.linspace(-0.1, 0.1, c1, device=dev)
+    xb = torch.relu(torch.randn(B, h, h, cin, device=dev, generator=g))
+    amb = ops.act_absmax(xb)
+    xbq = ops.act_quantize(xb, amb, 3)
+
+    def sep():
+        _, yd = ops.tuned_conv2d_q(xbq, amb, dcodes, None, 1, 1, 1, 0, dscale, dsh, emit_range=RNG, overflow=ovf,
+                                   want_f32=False)
+        _, y1 = ops.tuned_conv2d_q(xq, am, k1, None, 1, 1, 1, 0, cs1, sh1, relu=True, emit_range=RNG, overflow=ovf,
+                                   want_f32=False, residual_q=yd, residual_range=RNG)
+        out["sep"] = y1
+
+    def dsonly():
+        ops.tuned_conv2d_q(xbq, amb, dcodes, None, 1, 1, 1, 0, dscale, dsh, emit_range=RNG, overflow=ovf,
+                           want_f32=False)
+
+    def chain():
+        out["chain"] = ops.conv_chain_q(xq, am, k1, None, cs1, sh1, RNG, None, ovf,
+                                        ds=(xbq, amb, dcodes, dscale, dsh, RNG))[0]
+    t_sep, t_ds, t_chain = timed(sep), timed(dsonly), timed(chain)
+    print("B=%d ds %d->%d + conv3 %d->%d @%d: two launches %.1f us (downsample alone %.1f), chain %.1f us (%.2fx)%s"
+          % (B, cin, c1, cin, c1, h, t_sep, t_ds, t_chain, t_sep / t_chain,
+             "" if torch.equal(out["sep"], out["chain"]) else "  MISMATCH"), flush=True)
