@@ -225,21 +225,26 @@ int smpq_conv2d_pair_fwd(const int8_t* xq, const float* x_absmax, int n, int h, 
 /* ABI 7: the general form of the Bottleneck tail chain. conv3 (exact codes; offset1 = its weight
  * offsets or NULL) with its identity from ONE of
  *   residual_q / residual_range        the identity's limb planes, as smpq_conv2d_pair_fwd, or
- *   ds_xq [3][n*h*w][cin], ds_x_absmax [n], ds_codes [3][cout1][cin] (ds_wlimbs = 3: 24-bit fixed
- *   point from smpq_pack_weights_ex), ds_col_scale / ds_col_shift [cout1], ds_range
- *                                      the block's 1x1 / stride-1 downsample over the same pixels,
- *                                      computed in the same tiles: its clamped output codes (what a
+ *   ds_xq [3][n*ds_h*ds_w][ds_cin], ds_x_absmax [n], ds_codes [3][cout1][ds_cin] (ds_wlimbs = 3:
+ *   24-bit fixed point from smpq_pack_weights_ex), ds_col_scale / ds_col_shift [cout1], ds_range
+ *                                      the block's 1x1 downsample (stride ds_stride) whose output
+ *                                      pixels are conv3's, computed in the same tiles: its clamped
+ *                                      output codes (what a
  *                                      smpq_conv2d_fwd_q launch with emit range ds_range writes) are
  *                                      conv3's residual and are never written; overflow covers them,
  * and optionally (codes2 != NULL) the next block's conv1 on conv3's output as smpq_conv2d_pair_fwd
  * (no offsets). Every output and the overflow flag are bitwise those of the separate launches.
- * Built for conv3 64 -> 256 with cout2 = 64 or no second conv (smpq_conv2d_chain_supported with
- * cout2 = 0); other calls return SMPQ_E_INVALID. */
+ * Built: conv3 64 -> 256 with the next conv1 256 -> 64 (smpq_conv2d_chain_supported), and conv3
+ * with a fused downsample and no second conv for the first blocks of R50's layers 1-3 (64 -> 256 /
+ * ds 64 / stride 1, 128 -> 512 / ds 256 / 2, 256 -> 1024 / ds 512 / 2: smpq_conv2d_chain_ds_supported);
+ * other calls return SMPQ_E_INVALID. */
 int smpq_conv2d_chain_supported(int cin, int cout1, int cout2, int limbs);
+int smpq_conv2d_chain_ds_supported(int cin, int cout1, int ds_cin, int ds_stride, int limbs);
 int smpq_conv2d_chain_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                           const int8_t* codes1, const int32_t* offset1, int cout1, const float* col_scale1,
                           const float* col_shift1, const int8_t* residual_q, float residual_range,
-                          const int8_t* ds_xq, const float* ds_x_absmax, const int8_t* ds_codes, int ds_wlimbs,
+                          const int8_t* ds_xq, const float* ds_x_absmax, int ds_h, int ds_w, int ds_cin,
+                          int ds_stride, const int8_t* ds_codes, int ds_wlimbs,
                           const float* ds_col_scale, const float* ds_col_shift, float ds_range, int8_t* yq1,
                           float yq1_range, const float* y1_absmax, const int8_t* codes2, int cout2,
                           const float* col_scale2, const float* col_shift2, int8_t* yq2, float yq2_range,

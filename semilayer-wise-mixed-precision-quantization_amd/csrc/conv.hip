@@ -641,10 +641,15 @@ extern "C" int smpq_conv2d_chain_supported(int cin, int cout1, int cout2, int li
   return resident_pair_supported(cin, cout1, cout2, limbs) ? 1 : 0;
 }
 
+extern "C" int smpq_conv2d_chain_ds_supported(int cin, int cout1, int ds_cin, int ds_stride, int limbs) {
+  return resident_chain_ds_supported(cin, cout1, ds_cin, ds_stride, limbs) ? 1 : 0;
+}
+
 extern "C" int smpq_conv2d_chain_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                                      const int8_t* codes1, const int32_t* offset1, int cout1, const float* col_scale1,
                                      const float* col_shift1, const int8_t* residual_q, float residual_range,
-                                     const int8_t* ds_xq, const float* ds_x_absmax, const int8_t* ds_codes,
+                                     const int8_t* ds_xq, const float* ds_x_absmax, int ds_h, int ds_w,
+                                     int ds_cin, int ds_stride, const int8_t* ds_codes,
                                      int ds_wlimbs, const float* ds_col_scale, const float* ds_col_shift,
                                      float ds_range, int8_t* yq1, float yq1_range, const float* y1_absmax,
                                      const int8_t* codes2, int cout2, const float* col_scale2,
@@ -666,8 +671,9 @@ extern "C" int smpq_conv2d_chain_fwd(const int8_t* xq, const float* x_absmax, in
     a.res_scale = ds_range / 8323072.f;
     // the downsample as its own launch would run it (its output quantizer: yq1 stands in for the
     // planes it would write; the chain never writes them)
-    rc = conv_args_q(ds_xq, ds_x_absmax, n, h, w, cin, ds_codes, 3, nullptr, cout1, 1, 1, 1, 0, ds_col_scale,
-                     ds_col_shift, nullptr, 0, limbs, nullptr, nullptr, yq1, ds_range, overflow, nullptr, 0.f, d);
+    rc = conv_args_q(ds_xq, ds_x_absmax, n, ds_h, ds_w, ds_cin, ds_codes, 3, nullptr, cout1, 1, 1, ds_stride, 0,
+                     ds_col_scale, ds_col_shift, nullptr, 0, limbs, nullptr, nullptr, yq1, ds_range, overflow, nullptr,
+                     0.f, d);
     if (rc) return rc;
   }
   if (codes2) {
@@ -675,7 +681,8 @@ extern "C" int smpq_conv2d_chain_fwd(const int8_t* xq, const float* x_absmax, in
                      nullptr, 1, limbs, nullptr, nullptr, yq2, yq2_range, overflow, nullptr, 0.f, b);
     if (rc) return rc;
   }
-  const long long big = (long long)limbs * a.M * (cout1 > cin ? cout1 : cin);
+  long long big = (long long)limbs * a.M * (cout1 > cin ? cout1 : cin);
+  if (ds_xq && (long long)limbs * d.plane > big) big = (long long)limbs * d.plane;
   if (big > 0x7fffff00LL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_chain_fwd: a limb plane of 2 GiB or more");
   return launch_resident_chain(a, codes2 ? &b : nullptr, ds_xq ? &d : nullptr, limbs, (hipStream_t)stream);
 }
@@ -688,6 +695,6 @@ extern "C" int smpq_conv2d_pair_fwd(const int8_t* xq, const float* x_absmax, int
                                     float yq2_range, int32_t* overflow, smpq_stream_t stream) {
   if (!residual_q || !codes2) return fail(SMPQ_E_INVALID, "smpq_conv2d_pair_fwd: null pointer");
   return smpq_conv2d_chain_fwd(xq, x_absmax, n, h, w, cin, codes1, nullptr, cout1, col_scale1, col_shift1, residual_q,
-                               residual_range, nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0.f, yq1, yq1_range,
+                               residual_range, nullptr, nullptr, 0, 0, 0, 0, nullptr, 0, nullptr, nullptr, 0.f, yq1, yq1_range,
                                y1_absmax, codes2, cout2, col_scale2, col_shift2, yq2, yq2_range, overflow, stream);
 }

@@ -102,6 +102,7 @@ int launch_resident(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream
 bool glds_is_resident(int cfg);
 // the Bottleneck tail chains: conv3 (+ fused downsample) (-> next conv1) (smpq_conv2d_chain_fwd)
 bool resident_pair_supported(int cin, int cout1, int cout2, int limbs);
+bool resident_chain_ds_supported(int cin, int cout1, int ds_cin, int ds_stride, int limbs);
 int launch_resident_chain(const ConvArgs& a, const ConvArgs* b, const ConvArgs* d, int limbs, hipStream_t s);
 
 // The 4 codes (channels 0..3) held by one dword per limb plane, w[l] = the 4 balanced digits of

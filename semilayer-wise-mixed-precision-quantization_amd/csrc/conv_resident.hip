@@ -81,13 +81,15 @@ __device__ __forceinline__ int ach(int c, int r) {
   else return c ^ (r & 15);
 }
 
-template <int L, int LW, int KC, int CW, int WP, bool RES, int CW2 = 0, int LWD = 0, bool OFF = false>
+template <int L, int LW, int KC, int CW, int WP, bool RES, int CW2 = 0, int LWD = 0, bool OFF = false,
+          int KCD = KC>
 struct ResShape {
   static constexpr int SMIN = (L + LW - 4) > 0 ? (L + LW - 4) : 0;
   static constexpr int NACC = L + LW - 1 - SMIN;
   static constexpr int BN = 64 * CW, BP = 16 * WP, K = 64 * KC;
   static constexpr int ATILE = L * BP * K;                     // activation tile bytes
-  static constexpr int ASTAGE = ATILE * (LWD > 0 ? 2 : 1);     // + the fused downsample's tile
+  static constexpr int ATILE_D = LWD > 0 ? L * BP * 64 * KCD : 0;  // the fused downsample's tile
+  static constexpr int ASTAGE = ATILE + ATILE_D;
   static constexpr int OTILE = L * BP * BN;  // output (and residual) tile bytes
   static constexpr int OTILE2 = L * BP * 64 * CW2;  // the chained conv's output tile
   static constexpr int LDS = 2 * ASTAGE + (RES ? 3 : 1) * OTILE + OTILE2;
@@ -96,7 +98,7 @@ struct ResShape {
   // (+ the fused downsample's accumulators and epilogue constants; the offsets and digit sums: the
   // compiler's counts, tools/ resource usage, need this much margin to stay spill-free)
   static constexpr int NACC_D = LWD > 0 ? L + LWD - 1 - ((L + LWD - 4) > 0 ? (L + LWD - 4) : 0) : 0;
-  static constexpr int REGS = 4 * (LW * KC * CW + CW * CW2 + LWD * KC * CW + NACC * CW * WP + L * WP) + 40 +
+  static constexpr int REGS = 4 * (LW * KC * CW + CW * CW2 + LWD * KCD * CW + NACC * CW * WP + L * WP) + 40 +
                               (LWD > 0 ? 8 * CW + 4 * CW * WP + (CW2 > 0 ? 4 * NACC_D * CW * WP : 0) : 0) +
                               (OFF ? 8 * CW + L * WP : 0);
   // workgroups per CU (1 wave per SIMD each; past 256 the accumulators move to AGPRs)
@@ -109,10 +111,10 @@ struct ResShape {
 };
 
 template <int L, int LW, int KC, int CW, int WP, bool RELU, bool RES, int MINW, int CW2 = 0, bool OFF = false,
-          int LWD = 0>
+          int LWD = 0, int KCD = KC>
 __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvArgs a, ConvArgs b, ConvArgs d,
                                                                            int ntiles, int nslabs) {
-  using S = ResShape<L, LW, KC, CW, WP, RES, CW2, LWD, OFF>;
+  using S = ResShape<L, LW, KC, CW, WP, RES, CW2, LWD, OFF, KCD>;
   constexpr int SMIN = S::SMIN, NACC = S::NACC, BN = S::BN, BP = S::BP, K = S::K, ASTAGE = S::ASTAGE;
   constexpr int ATILE = S::ATILE;
   static_assert(!OFF || (LW == 1 && SMIN == 0), "weight offsets: exact codes only");
@@ -175,19 +177,20 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
         wb[kc][i] = v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
       }
   }
-  // the fused downsample's weight limbs (LWD > 0: same slab, same K)
-  v4i wd[LWD > 0 ? LWD : 1][LWD > 0 ? KC : 1][LWD > 0 ? CW : 1];
+  // the fused downsample's weight limbs (LWD > 0: same slab, K = 64 KCD)
+  constexpr int KD = 64 * KCD;
+  v4i wd[LWD > 0 ? LWD : 1][LWD > 0 ? KCD : 1][LWD > 0 ? CW : 1];
   if constexpr (LWD > 0) {
     const auto wrsd = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(d.codes), 0, (int)(LWD * d.wplane), 0x00020000);
 #pragma unroll
     for (int lw = 0; lw < LWD; ++lw)
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc)
+      for (int kc = 0; kc < KCD; ++kc)
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
           const int row = n0 + (wave * CW + i) * 16 + frow;
           const unsigned off = d.w_kmajor ? (unsigned)(kc * d.cout * 64 + row * 64 + 16 * grp)
-                                          : (unsigned)(row * K + kc * 64 + 16 * grp);
+                                          : (unsigned)(row * KD + kc * 64 + 16 * grp);
           const v4u v = __builtin_amdgcn_raw_buffer_load_b128(wrsd, off, (unsigned)(lw * d.wplane), 0);
           wd[lw][kc][i] = v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
         }
@@ -198,12 +201,13 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
   const v4i xrs = make_rsrc(a.xq, (long long)L * a.plane);
   const v4i xrsd = make_rsrc(LWD > 0 ? d.xq : nullptr, LWD > 0 ? (long long)L * d.plane : 0);
   const int hw_out = a.ho * a.wo;
+  // the fused downsample's tile: the same output pixels, sampled from its own input (h, w, stride,
+  // K = KD); piece = RPD rows x KD bytes
+  constexpr int CHD = KD / 16, RPD = 1024 / KD, DPIECES = LWD > 0 ? L * BP / RPD : 0;
+  const int prowd = lane / CHD, pphysd = lane % CHD;
   auto issue_acts = [&](int t, int stage) {
-    for (int p = wave; p < (LWD > 0 ? 2 : 1) * APIECES; p += 4) {
-      // pieces APIECES.. : the fused downsample's tile (the same pixels, addressing and K)
-      const bool dsp = LWD > 0 && p >= APIECES;
-      const int pp = dsp ? p - APIECES : p;
-      const int l = pp / (BP / RP), r = (pp % (BP / RP)) * RP + prow;  // tile row (pixel) of this lane
+    for (int p = wave; p < APIECES; p += 4) {
+      const int l = p / (BP / RP), r = (p % (BP / RP)) * RP + prow;  // tile row (pixel) of this lane
       const int m = t * BP + r;
       unsigned src = kOOB;
       if (m < a.M) {
@@ -212,11 +216,22 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
         const int oh = fast_div(rem, a.wo_mul, a.wo_shr), ow = rem - oh * a.wo;
         src = (unsigned)(((img * a.h + oh * a.stride) * a.w + ow * a.stride) * K + 16 * ach<KC>(pphys, r));
       }
-      if (dsp)
-        dma16(lds0 + stage * ASTAGE + ATILE + pp * 1024, xrsd, src,
+      dma16(lds0 + stage * ASTAGE + p * 1024, xrs, src, __builtin_amdgcn_readfirstlane((unsigned)((long long)l * a.plane)));
+    }
+    if constexpr (LWD > 0) {
+      for (int p = wave; p < DPIECES; p += 4) {
+        const int l = p / (BP / RPD), r = (p % (BP / RPD)) * RPD + prowd;
+        const int m = t * BP + r;
+        unsigned src = kOOB;
+        if (m < a.M) {
+          const int img = fast_div(m, a.hw_mul, a.hw_shr);
+          const int rem = m - img * hw_out;
+          const int oh = fast_div(rem, a.wo_mul, a.wo_shr), ow = rem - oh * a.wo;
+          src = (unsigned)(((img * d.h + oh * d.stride) * d.w + ow * d.stride) * KD + 16 * ach<KCD>(pphysd, r));
+        }
+        dma16(lds0 + stage * ASTAGE + ATILE + p * 1024, xrsd, src,
               __builtin_amdgcn_readfirstlane((unsigned)((long long)l * d.plane)));
-      else
-        dma16(lds0 + stage * ASTAGE + p * 1024, xrs, src, __builtin_amdgcn_readfirstlane((unsigned)((long long)l * a.plane)));
+      }
     }
   };
   // the residual tile [L][BP][BN] of tile t (RES): piece = 1024 / BN rows x BN bytes of one limb, 16-B
@@ -366,14 +381,14 @@ __global__ __launch_bounds__(kResThreads, MINW) void qconv_resident_kernel(ConvA
     int dq[LWD > 0 ? CW : 1][LWD > 0 ? WP : 1][4];
     if constexpr (LWD > 0) {
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
+      for (int kc = 0; kc < KCD; ++kc) {
         v4i fd[L][WP];
 #pragma unroll
         for (int l = 0; l < L; ++l)
 #pragma unroll
           for (int j = 0; j < WP; ++j) {
             const int r = j * 16 + frow;
-            fd[l][j] = *reinterpret_cast<const v4i*>(as + ATILE + (l * BP + r) * K + 16 * ach<KC>(4 * kc + grp, r));
+            fd[l][j] = *reinterpret_cast<const v4i*>(as + ATILE + (l * BP + r) * KD + 16 * ach<KCD>(4 * kc + grp, r));
           }
 #pragma unroll
         for (int l = 0; l < L; ++l)
@@ -640,11 +655,11 @@ int launch_res_l(int cfg, const ConvArgs& a, hipStream_t s) {
 // the Bottleneck tail chain: conv3 (one slab with all its output channels, 16-pixel tiles) with
 // its identity as limb planes (LWD == 0) or as the fused downsample (LWD == 3), optionally the next
 // block's conv1 (CW2 > 0), conv3's weight offsets or not
-template <int L, int KC, int CW, int CW2, bool OFF, int LWD>
+template <int L, int KC, int CW, int CW2, bool OFF, int LWD, int KCD = KC>
 int launch_chain_one(const ConvArgs& a, const ConvArgs& b, const ConvArgs& d, hipStream_t s) {
-  using S = ResShape<L, 1, KC, CW, 1, LWD == 0, CW2, LWD, OFF>;
+  using S = ResShape<L, 1, KC, CW, 1, LWD == 0, CW2, LWD, OFF, KCD>;
   static_assert(S::MINW >= 1, "LDS per CU");
-  auto k = qconv_resident_kernel<L, 1, KC, CW, 1, true, LWD == 0, S::MINW, CW2, OFF, LWD>;
+  auto k = qconv_resident_kernel<L, 1, KC, CW, 1, true, LWD == 0, S::MINW, CW2, OFF, LWD, KCD>;
   static const hipError_t attr = [&] {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS_TOTAL);
@@ -716,14 +731,28 @@ bool resident_pair_supported(int cin, int cout1, int cout2, int limbs) {
   return limbs == 3 && cin == 64 && cout1 == 256 && (cout2 == 64 || cout2 == 0);
 }
 
+// conv3 (cin -> cout1) with a fused 1x1 downsample (ds_cin -> cout1, stride ds_stride) and no chained
+// conv1: the first Bottleneck of R50's layer1 (64 -> 256, downsample 64 -> 256 / 1), layer2 (128 ->
+// 512, downsample 256 -> 512 / 2) and layer3 (256 -> 1024, downsample 512 -> 1024 / 2)
+bool resident_chain_ds_supported(int cin, int cout1, int ds_cin, int ds_stride, int limbs) {
+  return limbs == 3 && ((cin == 64 && cout1 == 256 && ds_cin == 64 && ds_stride == 1) ||
+                        (cin == 128 && cout1 == 512 && ds_cin == 256 && ds_stride == 2) ||
+                        (cin == 256 && cout1 == 1024 && ds_cin == 512 && ds_stride == 2));
+}
+
 int launch_resident_chain(const ConvArgs& a, const ConvArgs* b, const ConvArgs* d, int limbs, hipStream_t s) {
   auto conv1x1 = [](const ConvArgs& c) { return c.kh == 1 && c.kw == 1 && c.stride == 1 && c.pad == 0 && !c.s2d; };
-  if (!resident_pair_supported(a.cin, a.cout, b ? b->cout : 0, limbs) || !conv1x1(a) ||
-      (b && (!conv1x1(*b) || b->cin != a.cout || b->M != a.M)) ||
-      (d && (!conv1x1(*d) || d->cin != a.cin || d->cout != a.cout || d->h != a.h || d->w != a.w || d->n != a.n)))
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_chain_fwd: shapes not built (conv3 64->256 1x1 stride 1, 3 activation "
-                                "limbs; the next conv1 256->64 on its output; a downsample 64->256 1x1 stride 1 on "
-                                "the same pixels)");
+  auto ds1x1 = [](const ConvArgs& c) { return c.kh == 1 && c.kw == 1 && c.pad == 0 && !c.s2d; };
+  const bool shapes_ok =
+      conv1x1(a) && (d ? resident_chain_ds_supported(a.cin, a.cout, d->cin, d->stride, limbs) && ds1x1(*d) &&
+                             d->cout == a.cout && d->ho == a.ho && d->wo == a.wo && d->n == a.n
+                       : resident_pair_supported(a.cin, a.cout, b ? b->cout : 0, limbs)) &&
+      (!b || (conv1x1(*b) && b->cin == a.cout && b->M == a.M));
+  if (!shapes_ok)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_chain_fwd: shapes not built (conv3 1x1 stride 1, 3 activation limbs: "
+                                "64->256 with the next conv1 256->64 on its output, or with its downsample over the "
+                                "same output pixels: 64->256 / 1, 256->512 / 2 under 128->512, 512->1024 / 2 under "
+                                "256->1024)");
   if (!a.yq || a.y || a.residual || a.y_absmax || !a.relu || (!a.res_q) == (d == nullptr) ||
       (b && (!b->yq || b->y || b->residual || b->res_q || b->y_absmax || b->has_offset || !b->relu ||
              b->overflow != a.overflow)) ||
@@ -738,6 +767,9 @@ int launch_resident_chain(const ConvArgs& a, const ConvArgs* b, const ConvArgs* 
     // conv1 as well it needs one 256-channel slab, ~410 registers per lane and one workgroup per
     // CU: measured 4-5 % slower on the R50 step than without (profiles/r06_chain_fused_ds.txt); not built
     if (b) return fail(SMPQ_E_INVALID, "smpq_conv2d_chain_fwd: the fused downsample is built without a chained conv1");
+    // (layer2 / layer3: 128- / 64-channel slabs, the downsample's K 256 / 512 beside conv3's 128 / 256)
+    if (a.cin == 128) return off ? launch_chain_one<3, 2, 2, 0, true, 3, 4>(a, bb, dd, s) : launch_chain_one<3, 2, 2, 0, false, 3, 4>(a, bb, dd, s);
+    if (a.cin == 256) return off ? launch_chain_one<3, 4, 1, 0, true, 3, 8>(a, bb, dd, s) : launch_chain_one<3, 4, 1, 0, false, 3, 8>(a, bb, dd, s);
     return off ? launch_chain_one<3, 1, 2, 0, true, 3>(a, bb, dd, s) : launch_chain_one<3, 1, 2, 0, false, 3>(a, bb, dd, s);
   }
   if (!b) return fail(SMPQ_E_INVALID, "smpq_conv2d_chain_fwd: nothing to chain (plain conv3: smpq_conv2d_fwd_q)");

@@ -56,8 +56,10 @@ _PROTOS = {
     "smpq_weights_kmajor": (_i, [_vp, _i, _i, _i, _vp, _vp]),
     "smpq_conv2d_pair_supported": (_i, [_i] * 4),
     "smpq_conv2d_chain_supported": (_i, [_i] * 4),
+    "smpq_conv2d_chain_ds_supported": (_i, [_i] * 5),
     "smpq_conv2d_chain_fwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, ctypes.c_float,
-                                   _vp, _vp, _vp, _i, _vp, _vp, ctypes.c_float, _vp, ctypes.c_float, _vp,
+                                   _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, ctypes.c_float, _vp,
+                                   ctypes.c_float, _vp,
                                    _vp, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _vp]),
     "smpq_conv2d_pair_fwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, ctypes.c_float, _vp,
                                   ctypes.c_float, _vp, _vp, _i, _vp, _vp, _vp, ctypes.c_float, _vp, _vp]),

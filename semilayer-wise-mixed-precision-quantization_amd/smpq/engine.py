@@ -76,6 +76,8 @@ PAIR_1X1 = [_os.environ.get("SMPQ_PAIR_1X1", "1") != "0"]
 # static range: a stage's first Bottleneck computes its 1x1 / stride-1 downsample inside conv3's
 # tiles (ops.conv_chain_q; its output limb planes are never written) where that is built
 FUSE_DS = [_os.environ.get("SMPQ_FUSE_DS", "1") != "0"]
+# ... for the blocks whose conv3 has at most this many input channels (64: layer1, 128: + layer2)
+FUSE_DS_MAX_CIN = [int(_os.environ.get("SMPQ_FUSE_DS_MAX_CIN", "256"))]
 stats.setdefault("graph_captures", 0)
 stats.setdefault("graph_replays", 0)
 
@@ -287,21 +289,25 @@ def _pair_plan(blk, nxt, ctx):
 
 def _ds_fuse_plan(blk, x, ctx):
     """The downsample's plan when it can run inside blk.conv3's tiles (ops.conv_chain_q): a
-    Bottleneck whose conv1 / conv2 keep the resolution, a 1x1 / stride-1 downsample conv + BN over
-    conv3's K and output channels in 24-bit fixed point, static ranges for both, a built shape."""
+    Bottleneck whose downsample (1x1 conv + BN, 24-bit fixed point) has the stride of its conv2
+    (so its output pixels are conv3's), static ranges for both, a built shape
+    (ops.conv_chain_ds_supported)."""
     if not (FUSE_DS[0] and ctx is not None and ctx.ranges is not None and hasattr(blk, "conv3")
             and isinstance(blk.downsample, torch.nn.Sequential) and len(blk.downsample) == 2
             and x.q is not None and x.amax is not None and x.q.shape[0] == 3):
         return None
     dc, dbn, c3 = blk.downsample[0], blk.downsample[1], blk.conv3
-    if not (isinstance(dbn, torch.nn.BatchNorm2d) and _1x1(dc) and _1x1(c3) and blk.conv1.stride == (1, 1)
-            and blk.conv2.stride == (1, 1) and dc.in_channels == c3.in_channels
-            and dc.out_channels == c3.out_channels and id(dc) in ctx.ranges and id(c3) in ctx.ranges):
+    st = dc.stride[0]
+    if not (isinstance(dbn, torch.nn.BatchNorm2d) and dc.kernel_size == (1, 1) and dc.padding == (0, 0)
+            and dc.groups == 1 and dc.stride == (st, st) and _1x1(c3) and blk.conv1.stride == (1, 1)
+            and c3.in_channels <= FUSE_DS_MAX_CIN[0]
+            and blk.conv2.stride == (st, st) and dc.out_channels == c3.out_channels
+            and id(dc) in ctx.ranges and id(c3) in ctx.ranges):
         return None
     pd, p3 = conv_plan(dc, dbn), conv_plan(c3, blk.bn3)
     if pd is None or not _exact(p3) or pd[1] is not None or pd[0].dim() != 3 or pd[0].shape[0] != 3:
         return None
-    if not ops.conv_chain_supported(c3.in_channels, c3.out_channels, 0):
+    if not ops.conv_chain_ds_supported(c3.in_channels, c3.out_channels, dc.in_channels, st):
         return None
     return pd
 
@@ -367,8 +373,10 @@ def block_forward(blk, x, ctx=None, last=False, t1=None, nxt=None):
         p1 = None if (last or dsplan is not None) else _pair_plan(blk, nxt, ctx)
         ident_q = dsplan is not None or (isinstance(identity, Act) and identity.f32 is None
                                          and identity.q is not None and identity.rng is not None)
+        st = blk.downsample[0].stride[0] if dsplan is not None else 1
         chain = (dsplan is not None or p1 is not None) and ident_q and t2.q is not None and t2.amax is not None \
-            and t2.q.shape[0] == 3 and (dsplan is None or t2.q.shape[1:4] == x.q.shape[1:4])
+            and t2.q.shape[0] == 3 and (dsplan is None or t2.q.shape[2:4] == tuple((d - 1) // st + 1
+                                                                                    for d in x.q.shape[2:4]))
         if dsplan is not None and not chain:
             identity = as_identity(downsample())  # (not expected: conv2 ran outside the static path)
         if chain:
@@ -379,7 +387,7 @@ def block_forward(blk, x, ctx=None, last=False, t1=None, nxt=None):
             dsarg = nxtarg = None
             if dsplan is not None:
                 dcodes, _, dcs, dsh, dkind = dsplan
-                dsarg = (x.q, x.amax, dcodes, dcs, dsh, ctx.ranges[id(blk.downsample[0])])
+                dsarg = (x.q, x.amax, dcodes, dcs, dsh, ctx.ranges[id(blk.downsample[0])], st)
             if p1 is not None:
                 nxtarg = (p1[0], p1[2], p1[3], ctx.ranges[id(nxt.conv1)])
             yq3, yq1 = ops.conv_chain_q(t2.q, t2.amax, codes3, off3, cs3, sh3, rng3, am3, ctx.overflow,
@@ -722,7 +730,7 @@ def _graph_base(cal):
     """What every captured graph of a model depends on besides its input's shape and address:
     the calibration (ranges, signature) and the forward's structure knobs."""
     return (cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0], CONCURRENT_DS[0], STREAMS[0],
-            ops.KMAJOR[0], PAIR_1X1[0], FUSE_DS[0])
+            ops.KMAJOR[0], PAIR_1X1[0], FUSE_DS[0], FUSE_DS_MAX_CIN[0])
 
 
 def _graph_key(model, x, cal):

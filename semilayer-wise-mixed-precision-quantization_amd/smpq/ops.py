@@ -512,6 +512,13 @@ def conv_chain_supported(cin, cout1, cout2=0, limbs=3):
     return bool(_lib.load().smpq_conv2d_chain_supported(int(cin), int(cout1), int(cout2), int(limbs)))
 
 
+def conv_chain_ds_supported(cin, cout1, ds_cin, ds_stride, limbs=3):
+    """Does smpq_conv2d_chain_fwd run conv3 cin -> cout1 with a fused 1x1 downsample ds_cin ->
+    cout1 of this stride (and no chained conv1)?"""
+    return bool(_lib.load().smpq_conv2d_chain_ds_supported(int(cin), int(cout1), int(ds_cin), int(ds_stride),
+                                                           int(limbs)))
+
+
 def _one_limb(codes, what):
     _req(codes.dim() == 2 or codes.shape[0] == 1, "chain: %s needs exact codes (one weight limb)" % what)
     return codes[0] if codes.dim() == 3 else codes
@@ -522,9 +529,9 @@ def conv_chain_q(xq, x_absmax, codes1, offset1, col_scale1, col_shift1, emit_ran
     """A Bottleneck's conv3 (1x1 + folded BN + identity + ReLU, exact codes, optional weight offsets)
     in one launch with (csrc/conv_resident.hip, smpq_conv2d_chain_fwd):
       - its identity: ``residual_q`` limb planes (+ ``residual_range``), or ``ds`` = (ds_xq,
-        ds_x_absmax, ds_codes [3, cout1, cin], ds_col_scale, ds_col_shift, ds_range): the block's 1x1
-        stride-1 downsample computed in the same tiles (its output codes feed the residual; never
-        written);
+        ds_x_absmax, ds_codes [3, cout1, ds_cin], ds_col_scale, ds_col_shift, ds_range[, ds_stride]):
+        the block's 1x1 downsample (stride 1 by default) over conv3's output pixels, computed in the
+        same tiles (its output codes feed the residual; never written);
       - ``nxt`` = (codes2, col_scale2, col_shift2, emit_range2): the next block's conv1 (ReLU) on
         conv3's output tile.
     Returns (yq1, yq2 or None), bitwise what the separate launches write; ``overflow`` covers every
@@ -538,7 +545,12 @@ def conv_chain_q(xq, x_absmax, codes1, offset1, col_scale1, col_shift1, emit_ran
     _req(c1.shape == (cout1, cin) and c1.is_contiguous() and c1.dtype == torch.int8, "chain: conv3 codes")
     _req(c2 is None or (c2.shape == (cout2, cout1) and c2.is_contiguous() and c2.dtype == torch.int8),
          "chain: conv1 codes")
-    _req(conv_chain_supported(cin, cout1, cout2, limbs), "chain: shape not built")
+    ds_stride = int(ds[6]) if (ds is not None and len(ds) > 6) else 1
+    if ds is not None:
+        _req(cout2 == 0 and conv_chain_ds_supported(cin, cout1, ds[0].shape[-1], ds_stride, limbs),
+             "chain: shape not built")
+    else:
+        _req(conv_chain_supported(cin, cout1, cout2, limbs), "chain: shape not built")
     _req((residual_q is None) != (ds is None), "chain: one identity source (residual_q or ds)")
     _req(offset1 is None or (offset1.dtype == torch.int32 and offset1.numel() == cout1), "chain: offset")
     if residual_q is not None:
@@ -546,11 +558,13 @@ def conv_chain_q(xq, x_absmax, codes1, offset1, col_scale1, col_shift1, emit_ran
              and residual_q.is_contiguous() and residual_range is not None and residual_range > 0, "chain: residual_q")
     vecs = [(col_scale1, cout1), (col_shift1, cout1)]
     if ds is not None:
-        dxq, dam, dcodes, dcs, dsh, drng = ds
-        _req(dxq.shape == xq.shape and dxq.dtype == torch.int8 and dxq.is_contiguous() and dam.numel() == n,
-             "chain: downsample input")
-        _req(dcodes.shape == (3, cout1, cin) and dcodes.dtype == torch.int8 and dcodes.is_contiguous(),
-             "chain: downsample codes [3, cout, cin]")
+        dxq, dam, dcodes, dcs, dsh, drng = ds[:6]
+        _, _, dh, dw, dcin = dxq.shape
+        _req(dxq.dim() == 5 and dxq.shape[:2] == (limbs, n) and (dh - 1) // ds_stride + 1 == h
+             and (dw - 1) // ds_stride + 1 == w and dxq.dtype == torch.int8 and dxq.is_contiguous()
+             and dam.numel() == n, "chain: downsample input (its output pixels must be conv3's)")
+        _req(dcodes.shape == (3, cout1, dcin) and dcodes.dtype == torch.int8 and dcodes.is_contiguous(),
+             "chain: downsample codes [3, cout, ds_cin]")
         _req(drng > 0, "chain: downsample range")
         vecs += [(dcs, cout1), (dsh, cout1)]
     if nxt is not None:
@@ -561,7 +575,8 @@ def conv_chain_q(xq, x_absmax, codes1, offset1, col_scale1, col_shift1, emit_ran
              "chain: col vectors")
     _req(x_absmax.numel() == n and overflow is not None and overflow.dtype == torch.int32
          and overflow.device == xq.device, "chain: absmax / overflow")
-    nchunk = PLANE_LIMIT // (limbs * h * w * max(cin, cout1))
+    nchunk = PLANE_LIMIT // (limbs * max(h * w * max(cin, cout1), 0 if ds is None else ds[0].shape[2] * ds[0].shape[3]
+                                         * ds[0].shape[4]))
     _req(nchunk >= 1, "chain: one image's planes exceed 2 GiB")
     if n > nchunk:  # 32-bit buffer offsets: image chunks (independent images, the same result)
         yq1 = torch.empty(limbs, n, h, w, cout1, dtype=torch.int8, device=xq.device)
@@ -589,7 +604,9 @@ def conv_chain_q(xq, x_absmax, codes1, offset1, col_scale1, col_shift1, emit_ran
         _lib.check(lib.smpq_conv2d_chain_fwd(
             P(xq), P(x_absmax), n, h, w, cin, P(c1), P(offset1), cout1, P(col_scale1), P(col_shift1),
             P(residual_q), float(residual_range or 0.0),
-            P(ds[0]) if ds else None, P(ds[1]) if ds else None, P(ds[2]) if ds else None, 3 if ds else 0,
+            P(ds[0]) if ds else None, P(ds[1]) if ds else None, ds[0].shape[2] if ds else 0,
+            ds[0].shape[3] if ds else 0, ds[0].shape[4] if ds else 0, ds_stride if ds else 0,
+            P(ds[2]) if ds else None, 3 if ds else 0,
             P(ds[3]) if ds else None, P(ds[4]) if ds else None, float(ds[5]) if ds else 0.0,
             P(yq1), float(emit_range1), P(y1_absmax),
             P(c2), cout2, P(nxt[1]) if nxt else None, P(nxt[2]) if nxt else None, P(yq2),
@@ -599,7 +616,8 @@ def conv_chain_q(xq, x_absmax, codes1, offset1, col_scale1, col_shift1, emit_ran
         w1 = alg_work(n, h, w, cin, cout1, 1, 1, h, w, limbs, 1, False, True, False, residual_q is not None)
         ops_, nbytes, shape = w1["ops"], w1["bytes"], "%4d->%4d" % (cin, cout1)
         if ds is not None:
-            wd = alg_work(n, h, w, cin, cout1, 1, 1, h, w, limbs, 3, False, False, False, False)
+            wd = alg_work(n, ds[0].shape[2], ds[0].shape[3], ds[0].shape[4], cout1, 1, 1, h, w, limbs, 3, False,
+                          False, False, False)
             ops_ += wd["ops"]
             nbytes += wd["bytes"]  # the downsample's input and weights (its output never leaves the CU)
             shape += "+ds"
