@@ -212,8 +212,9 @@ int smpq_conv2d_fwd_q_km(const int8_t* xq, const float* x_absmax, int n, int h, 
  *   codes2 [cout2][cout1], col_scale2, col_shift2 [cout2]      the next block's conv1
  *   yq2 [3][n*h*w][cout2], yq2_range    conv1's output limb planes
  *   overflow                            int32 [1]: set when either output exceeded its range
- * Built for (cin, cout1, cout2) = (64, 256, 64), the ResNet-50 layer1 blocks
- * (smpq_conv2d_pair_supported); other calls return SMPQ_E_INVALID. */
+ * Built for (cin, cout1, cout2) = (64, 256, 64) and (64, 256, 128), the ResNet-50 layer1 blocks and
+ * layer 1's last conv3 with layer 2's first conv1 (smpq_conv2d_pair_supported); other calls return
+ * SMPQ_E_INVALID. */
 int smpq_conv2d_pair_supported(int cin, int cout1, int cout2, int limbs);
 int smpq_conv2d_pair_fwd(const int8_t* xq, const float* x_absmax, int n, int h, int w, int cin,
                          const int8_t* codes1, int cout1, const float* col_scale1, const float* col_shift1,
@@ -234,7 +235,7 @@ int smpq_conv2d_pair_fwd(const int8_t* xq, const float* x_absmax, int n, int h, 
  *                                      conv3's residual and are never written; overflow covers them,
  * and optionally (codes2 != NULL) the next block's conv1 on conv3's output as smpq_conv2d_pair_fwd
  * (no offsets). Every output and the overflow flag are bitwise those of the separate launches.
- * Built: conv3 64 -> 256 with the next conv1 256 -> 64 (smpq_conv2d_chain_supported), and conv3
+ * Built: conv3 64 -> 256 with the next conv1 256 -> 64 or 256 -> 128 (smpq_conv2d_chain_supported), and conv3
  * with a fused downsample and no second conv for the first blocks of R50's layers 1-3 (64 -> 256 /
  * ds 64 / stride 1, 128 -> 512 / ds 256 / 2, 256 -> 1024 / ds 512 / 2: smpq_conv2d_chain_ds_supported);
  * other calls return SMPQ_E_INVALID. */

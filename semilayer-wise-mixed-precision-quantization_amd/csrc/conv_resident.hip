@@ -100,7 +100,7 @@ struct ResShape {
   static constexpr int NACC_D = LWD > 0 ? L + LWD - 1 - ((L + LWD - 4) > 0 ? (L + LWD - 4) : 0) : 0;
   static constexpr int REGS = 4 * (LW * KC * CW + CW * CW2 + LWD * KCD * CW + NACC * CW * WP + L * WP) + 40 +
                               (LWD > 0 ? 8 * CW + 4 * CW * WP + (CW2 > 0 ? 4 * NACC_D * CW * WP : 0) : 0) +
-                              (OFF ? 8 * CW + L * WP : 0);
+                              (OFF ? 8 * CW + L * WP : 0) + (CW2 > 0 ? 8 * CW2 + 4 * L * CW2 * WP : 0);
   // workgroups per CU (1 wave per SIMD each; past 256 the accumulators move to AGPRs)
   static constexpr int MINW_R = REGS <= 120 ? 4 : (REGS <= 152 ? 3 : (REGS <= 240 ? 2 : 1));
   // + the per-image input scales (x_absmax / QMAX) of each conv, staged once (kNTab images)
@@ -728,7 +728,8 @@ int launch_resident(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream
 // one 512-channel slab: 452 registers per lane, one workgroup per CU, measured 0.82-0.85x the two
 // launches and the R50 step 1.2 % slower: profiles/r06_pair_chain.txt; not built.)
 bool resident_pair_supported(int cin, int cout1, int cout2, int limbs) {
-  return limbs == 3 && cin == 64 && cout1 == 256 && (cout2 == 64 || cout2 == 0);
+  // cout2 = 64: the layer-1 blocks' conv1; 128: layer 2's first conv1 (on layer 1's last output)
+  return limbs == 3 && cin == 64 && cout1 == 256 && (cout2 == 64 || cout2 == 128 || cout2 == 0);
 }
 
 // conv3 (cin -> cout1) with a fused 1x1 downsample (ds_cin -> cout1, stride ds_stride) and no chained
@@ -773,6 +774,8 @@ int launch_resident_chain(const ConvArgs& a, const ConvArgs* b, const ConvArgs* 
     return off ? launch_chain_one<3, 1, 2, 0, true, 3>(a, bb, dd, s) : launch_chain_one<3, 1, 2, 0, false, 3>(a, bb, dd, s);
   }
   if (!b) return fail(SMPQ_E_INVALID, "smpq_conv2d_chain_fwd: nothing to chain (plain conv3: smpq_conv2d_fwd_q)");
+  if (b->cout == 128)
+    return off ? launch_chain_one<3, 1, 4, 2, true, 0>(a, bb, dd, s) : launch_chain_one<3, 1, 4, 2, false, 0>(a, bb, dd, s);
   return off ? launch_chain_one<3, 1, 4, 1, true, 0>(a, bb, dd, s) : launch_chain_one<3, 1, 4, 1, false, 0>(a, bb, dd, s);
 }
 

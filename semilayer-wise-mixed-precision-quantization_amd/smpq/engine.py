@@ -73,6 +73,8 @@ STREAMS = [int(_os.environ.get("SMPQ_STREAMS", "2"))]
 # static range: a Bottleneck's conv3 and the next block's conv1 as ONE launch where the pair kernel
 # is built (ops.conv_pair_q: conv1 reads conv3's output tile from LDS; bitwise the two launches)
 PAIR_1X1 = [_os.environ.get("SMPQ_PAIR_1X1", "1") != "0"]
+# ... also onto the conv1 of the next stage's first block (which has a downsample)
+PAIR_STAGE_ENTRY = [_os.environ.get("SMPQ_PAIR_STAGE_ENTRY", "1") != "0"]
 # static range: a stage's first Bottleneck computes its 1x1 / stride-1 downsample inside conv3's
 # tiles (ops.conv_chain_q; its output limb planes are never written) where that is built
 FUSE_DS = [_os.environ.get("SMPQ_FUSE_DS", "1") != "0"]
@@ -273,8 +275,10 @@ def _exact(plan):
 def _pair_plan(blk, nxt, ctx):
     """The next block's conv1 plan when it can be chained onto blk.conv3 (static ranges, exact
     codes without offsets, 1x1 / stride 1 / pad 0 both, a built shape), else None."""
+    # (the next block may have a downsample: it reads the block input, which conv3 writes anyway)
     if not (PAIR_1X1[0] and nxt is not None and ctx is not None and ctx.ranges is not None
-            and hasattr(blk, "conv3") and hasattr(nxt, "conv3") and nxt.downsample is None):
+            and hasattr(blk, "conv3") and hasattr(nxt, "conv3")
+            and (nxt.downsample is None or PAIR_STAGE_ENTRY[0])):
         return None
     c3, c1 = blk.conv3, nxt.conv1
     if id(c3) not in ctx.ranges or id(c1) not in ctx.ranges or not (_1x1(c3) and _1x1(c1)):
@@ -730,7 +734,7 @@ def _graph_base(cal):
     """What every captured graph of a model depends on besides its input's shape and address:
     the calibration (ranges, signature) and the forward's structure knobs."""
     return (cal[1], CHUNK[0], ops.get_act_limbs(), id(cal[0]), FUSED_STEM[0], CONCURRENT_DS[0], STREAMS[0],
-            ops.KMAJOR[0], PAIR_1X1[0], FUSE_DS[0], FUSE_DS_MAX_CIN[0])
+            ops.KMAJOR[0], PAIR_1X1[0], FUSE_DS[0], FUSE_DS_MAX_CIN[0], PAIR_STAGE_ENTRY[0])
 
 
 def _graph_key(model, x, cal):
