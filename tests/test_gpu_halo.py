@@ -18,7 +18,7 @@ def _halo_cfgs(ops, limbs, cin, cout):
 @pytest.mark.parametrize("relu", [True, False])
 @pytest.mark.parametrize("limbs", [2, 3])
 @pytest.mark.parametrize("shape", [(64, 64, 56, 56, 2), (128, 128, 28, 28, 3), (256, 256, 14, 14, 2),
-                                   (64, 128, 13, 17, 2), (192, 64, 9, 30, 1),
+                                   (64, 128, 13, 17, 2), (192, 64, 9, 30, 1), (64, 64, 13, 17, 3),
                                    # narrow images: 7 x 7 (an odd image count), width 16, narrower
                                    # than 7, a partial row tile
                                    (512, 512, 7, 7, 3), (64, 128, 9, 16, 2), (128, 64, 5, 6, 3)],
