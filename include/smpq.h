@@ -323,9 +323,10 @@ int smpq_conv2d_tile_config(int cfg, int* bm, int* bn, int* threads);
  *   SMPQ_TILE_LDS_DMA_K128     as SMPQ_TILE_LDS_DMA with 128-wide K steps: also cin % 128 == 0
  *   SMPQ_TILE_HALO3X3          (ABI 5) halo-patch 3x3 kernel: 3x3 / stride 1 / pad 1 convs with
  *                              cin % 64 == 0, cout % 64 == 0, one weight limb, 2 or 3 activation
- *                              limbs, static-range limb-plane output with ReLU only (yq set,
- *                              relu != 0; y, y_absmax, residual, residual_q NULL) — other calls
- *                              return SMPQ_E_INVALID.
+ *                              limbs, static-range limb-plane output with ReLU (yq set,
+ *                              relu != 0; y, y_absmax, residual NULL), optionally with a
+ *                              limb-plane residual_q (round 6) — other calls return
+ *                              SMPQ_E_INVALID.
  *                              Its configurations follow the LDS-DMA ones; BM = the tile's pixels
  *                              (TH x TW of one image), BN = 64.
  *   SMPQ_TILE_RESIDENT1X1      (ABI 6) weight-stationary 1x1 tiles: 1x1 / pad 0 convs with cin

@@ -52,11 +52,13 @@ namespace {
 
 constexpr int kHaloWB = 9 * 64 * 64;  // weight image per stage: [tap][64 couts][64 B]
 
+// the residual tile staged in LDS (RES): [L][16 ceil(px / 16)][64] limb bytes
+__host__ __device__ constexpr int halo_res_bytes(int L, int th, int tw) { return L * ((th * tw + 15) / 16) * 1024; }
 __host__ __device__ constexpr int halo_patch_bytes(int L, int th, int tw) {
   return (L * (th + 2) * (tw + 2) * 64 + 1023) / 1024 * 1024;  // whole DMA pieces
 }
 
-template <int L, int TH, int TW, int NWV, int WPF, int NST, bool OFF>
+template <int L, int TH, int TW, int NWV, int WPF, int NST, bool OFF, bool RES>
 __global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nct, int ntw, int tiles_img) {
   constexpr int PH = TH + 2, PW = TW + 2;
   constexpr int NPIX = TH * TW;
@@ -167,6 +169,51 @@ __global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nc
     for (int par = 0; par < 2; ++par) bpar[j][par] = kHaloWB + (r * PW + c) * 64 + 16 * (grp ^ (2 * ((r + par) & 1)));
   }
 
+  // RES: the limb-plane residual (BasicBlock conv2: + identity, then ReLU) — each lane's 4-channel
+  // words of its pixels, loaded now and decoded in the epilogue (latency under the K loop)
+  const long long oplane = (long long)a.M * a.cout;
+  unsigned qoff[WPF];
+#pragma unroll
+  for (int j = 0; j < WPF; ++j) {
+    const int oh = oh0 + pr0[j], ow = ow0 + pc0[j];
+    const bool ok = pr0[j] >= 0 && oh < a.ho && ow < a.wo;
+    qoff[j] = ok ? (unsigned)(((long long)(img * a.ho + oh) * a.wo + ow) * a.cout + ct * 64 + 16 * grp) : kOOB;
+  }
+  // the residual tile by LDS-DMA (whole 64-B pixel rows; when it fits beside the stages), else
+  // each lane's 4-channel words by buffer loads
+  constexpr int RPP = (NPIX + 15) / 16;  // 16-pixel pieces per limb
+  constexpr bool RES_LDS = RES && NST * (kHaloWB + PB) + halo_res_bytes(L, TH, TW) <= 160 * 1024;
+  const unsigned resoff = (unsigned)((nch < NST ? nch : NST) * STAGE);
+  unsigned rqw[RES ? 4 : 1][WPF][RES ? L : 1];
+  if constexpr (RES_LDS) {
+    const v4i rrs = make_rsrc(a.res_q, (long long)L * oplane);
+    const unsigned lds0r = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+#pragma unroll
+    for (int k = 0; k < (L * RPP + NWV - 1) / NWV; ++k) {
+      const int q = wave + NWV * k;
+      if (q < L * RPP) {
+        const int l = q / RPP, pt = (q - l * RPP) * 16 + (lane >> 2);
+        const int oh = oh0 + pt / TW, ow = ow0 + pt % TW;
+        const bool ok = pt < NPIX && oh < a.ho && ow < a.wo;
+        const unsigned src = ok ? (unsigned)(((long long)(img * a.ho + oh) * a.wo + ow) * a.cout + ct * 64 + 16 * (lane & 3))
+                                : kOOB;
+        dma16(lds0r + resoff + (unsigned)q * 1024u, rrs, src, __builtin_amdgcn_readfirstlane((unsigned)((long long)l * oplane)));
+      }
+    }
+  } else if constexpr (RES) {
+    const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.res_q), 0, (int)(L * oplane), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < WPF; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        // channels ct * 64 + 16 i + 4 grp .. + 3 of pixel j (qoff[j] points at block grp's 16)
+        const unsigned ro = qoff[j] != kOOB ? qoff[j] - 16u * (unsigned)grp + 16u * (unsigned)i + 4u * (unsigned)grp : kOOB;
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+          rqw[i][j][l] = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(rrs, ro, (unsigned)((long long)l * oplane), 0);
+      }
+  }
+
   v4i acc[L][4][WPF];  // set by the first chunk's first tap (an MFMA with a zero C operand)
   constexpr bool do_off = OFF;  // weight offsets (compile-time: no merged paths in the epilogue)
   int rs[L][WPF];
@@ -273,14 +320,6 @@ __global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nc
           for (int r = 0; r < 4; ++r) acc[l][i][j][r] += __mul24(cor[r], rs[l][j]);
     }
   }
-  const long long oplane = (long long)a.M * a.cout;
-  unsigned qoff[WPF];
-#pragma unroll
-  for (int j = 0; j < WPF; ++j) {
-    const int oh = oh0 + pr0[j], ow = ow0 + pc0[j];
-    const bool ok = pr0[j] >= 0 && oh < a.ho && ow < a.wo;
-    qoff[j] = ok ? (unsigned)(((long long)(img * a.ho + oh) * a.wo + ow) * a.cout + ct * 64 + 16 * grp) : kOOB;
-  }
   constexpr float qmax = act_qmax<L>();
   const float rscale = a.x_absmax[img] * a.inv_qmax;
   const float inv = a.yq_inv;
@@ -288,7 +327,7 @@ __global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nc
   constexpr bool relu = true;
   unsigned wq[4][WPF][L];
   float vmax = 0.f;
-  const int rq_dummy[4] = {0, 0, 0, 0};
+  const float rsq = RES ? a.res_scale * inv : 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = ct * 64 + 16 * i + 4 * grp;
@@ -301,7 +340,19 @@ __global__ __launch_bounds__(64 * NWV) void qconv_halo_kernel(ConvArgs a, int nc
       v4i accq[L];
 #pragma unroll
       for (int l = 0; l < L; ++l) accq[l] = acc[l][i][j];
-      const float m = lean_quad<L, L, 0>(accq, rscale, csq, shq, false, rq_dummy, 0.f, relu, lo, wq[i][j]);
+      int rqv[4] = {0, 0, 0, 0};
+      if constexpr (RES_LDS) {
+        // landed before the first chunk's barrier (the first vmcnt(0) covers this wave's DMA)
+        const int pt = 16 * (wave * WPF + j) + frow;
+        unsigned rw[L];
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+          rw[l] = *reinterpret_cast<const unsigned*>(lds + resoff + l * RPP * 1024 + pt * 64 + 16 * i + 4 * grp);
+        decode4<L>(rw, rqv);
+      } else if constexpr (RES) {
+        decode4<L>(rqw[i][j], rqv);
+      }
+      const float m = lean_quad<L, L, 0>(accq, rscale, csq, shq, RES, rqv, rsq, relu, lo, wq[i][j]);
       vmax = qoff[j] != kOOB ? fmaxf(vmax, m) : vmax;
     }
   }
@@ -326,22 +377,29 @@ int launch_halo_one(const ConvArgs& a, hipStream_t stream) {
   if (blocks > 0x7fffffffLL) return fail(SMPQ_E_SHAPE, "smpq_conv2d_fwd: grid too large");
   constexpr int stage = kHaloWB + halo_patch_bytes(L, TH, TW);
   const int nch = a.cin / 64;
-  const int lds_bytes = (nch < NST ? nch : NST) * stage;
-  constexpr int kMax = NST * stage;
-  static_assert(kMax <= 160 * 1024, "LDS per CU");
-  auto k0 = qconv_halo_kernel<L, TH, TW, NWV, WPF, NST, false>;
-  auto k1 = qconv_halo_kernel<L, TH, TW, NWV, WPF, NST, true>;
-  auto set_lds = [](const void* k) {
-    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kMax);
-    if (e != hipSuccess) (void)hipGetLastError();
-    return e;
-  };
-  static const hipError_t attr0 = set_lds(reinterpret_cast<const void*>(k0));
-  static const hipError_t attr1 = set_lds(reinterpret_cast<const void*>(k1));
-  const bool off = a.has_offset != 0;
-  if ((off ? attr1 : attr0) != hipSuccess) return check_hip(off ? attr1 : attr0, "qconv_halo_kernel LDS attribute");
-  auto k = off ? k1 : k0;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * NWV), lds_bytes, stream, a, nct, ntw, nth * ntw);
+  constexpr int kResB = halo_res_bytes(L, TH, TW);
+  constexpr bool kResLds = NST * stage + kResB <= 160 * 1024;  // the kernel's RES_LDS
+  const int lds_bytes = (nch < NST ? nch : NST) * stage + (a.res_q && kResLds ? kResB : 0);
+  constexpr int kMax = NST * stage + (kResLds ? kResB : 0);
+  static_assert(NST * stage <= 160 * 1024, "LDS per CU");
+  using KFn = decltype(&qconv_halo_kernel<L, TH, TW, NWV, WPF, NST, false, false>);
+  // [offsets][residual]
+  static const KFn fns[4] = {qconv_halo_kernel<L, TH, TW, NWV, WPF, NST, false, false>,
+                             qconv_halo_kernel<L, TH, TW, NWV, WPF, NST, false, true>,
+                             qconv_halo_kernel<L, TH, TW, NWV, WPF, NST, true, false>,
+                             qconv_halo_kernel<L, TH, TW, NWV, WPF, NST, true, true>};
+  static hipError_t attrs[4];
+  static const bool attrs_set = [] {
+    for (int i = 0; i < 4; ++i) {
+      attrs[i] = hipFuncSetAttribute(reinterpret_cast<const void*>(fns[i]), hipFuncAttributeMaxDynamicSharedMemorySize, kMax);
+      if (attrs[i] != hipSuccess) (void)hipGetLastError();
+    }
+    return true;
+  }();
+  (void)attrs_set;
+  const int vi = (a.has_offset != 0 ? 2 : 0) + (a.res_q ? 1 : 0);
+  if (attrs[vi] != hipSuccess) return check_hip(attrs[vi], "qconv_halo_kernel LDS attribute");
+  hipLaunchKernelGGL(fns[vi], dim3((unsigned)blocks), dim3(64 * NWV), lds_bytes, stream, a, nct, ntw, nth * ntw);
   return check_hip(hipGetLastError(), "qconv_halo_kernel launch");
 }
 
@@ -385,8 +443,9 @@ int launch_halo(int cfg, int limbs, int wlimbs, const ConvArgs& a, hipStream_t s
   if (!halo_supported(cfg, a.cin, a.cout, a.kh, a.kw, limbs, wlimbs) || a.stride != 1 || a.pad != 1 || a.s2d)
     return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: halo tiles take 3x3 / stride 1 / pad 1 convs with cin % 64 == 0, "
                                 "cout % 64 == 0 and one weight limb");
-  if (!a.yq || a.y || a.residual || a.res_q || a.y_absmax || !a.relu)
-    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: halo tiles run the static-range limb-plane epilogue with ReLU only");
+  if (!a.yq || a.y || a.residual || a.y_absmax || !a.relu)
+    return fail(SMPQ_E_INVALID, "smpq_conv2d_fwd: halo tiles run the static-range limb-plane epilogue with ReLU "
+                                "(and optionally a limb-plane residual) only");
   switch (limbs) {
     case 2: return launch_halo_l<2>(cfg, a, s);
     case 3: return launch_halo_l<3>(cfg, a, s);

@@ -788,9 +788,10 @@ def tuned_conv2d_q(xq, x_absmax, codes, offset, kh, kw, stride, pad, col_scale, 
                  residual=residual, relu=relu, y_absmax=y_absmax, out=out, tile_cfg=c,
                  emit_range=emit_range, overflow=overflow, want_f32=want_f32,
                  residual_q=residual_q, residual_range=residual_range)
-    # the halo tiles run only the static-range limb-plane epilogue with ReLU (stride 1 / pad 1 for
-    # now): the key does not carry relu / y_absmax, so other calls of a key never see them
-    halo_ok = bool(relu and emit_range is not None and not want_f32 and residual is None and residual_q is None
+    # the halo tiles run only the static-range limb-plane epilogue with ReLU, optionally with a
+    # limb-plane residual (stride 1 / pad 1 for now): the key does not carry relu / y_absmax, so
+    # other calls of a key never see them
+    halo_ok = bool(relu and emit_range is not None and not want_f32 and residual is None
                    and y_absmax is None and out is None and kh == 3 and kw == 3 and stride == 1 and pad == 1)
     # the weight-stationary 1x1 tiles: the static-range limb-plane epilogue, built for the
     # downsamples (3 weight limbs, no ReLU or residual) and for exact-code convs with ReLU + a

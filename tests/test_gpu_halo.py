@@ -55,6 +55,46 @@ def test_halo_equals_implicit_gemm(gpu, shape, limbs, relu):
                 assert torch.equal(ovf, ovf0), (c, frac, layout)
 
 
+@pytest.mark.parametrize("with_offset", [True, False])
+@pytest.mark.parametrize("limbs", [2, 3])
+@pytest.mark.parametrize("shape", [(64, 64, 56, 56, 2), (128, 128, 28, 28, 3), (256, 256, 14, 14, 2),
+                                   (512, 512, 7, 7, 3), (64, 128, 13, 17, 2)],
+                         ids=lambda s: "c%d_o%d_%dx%d_n%d" % s)
+def test_halo_residual_equals_implicit_gemm(gpu, shape, limbs, with_offset):
+    """BasicBlock conv2 (+ the identity as limb planes, then ReLU) on the halo tiles: the limb-plane
+    outputs and overflow flags equal the implicit-GEMM kernel's bit for bit, in range and
+    overflowing, with and without weight offsets."""
+    from smpq import ops
+    cin, cout, h, w, n = shape
+    wd, step, codes, offset = make_layer(gpu, cin, cout, 3, seed=cin + cout + w)
+    offset = offset if with_offset else None
+    g = torch.Generator().manual_seed(h + 7 * w)
+    x = torch.relu(torch.randn(n, h, w, cin, generator=g)).to(gpu)
+    am = ops.act_absmax(x)
+    xq = ops.act_quantize(x, am, limbs)
+    r = torch.relu(torch.randn(n, h, w, cout, generator=g)).to(gpu)
+    rrange = float(r.abs().max()) * 1.5
+    rq = ops.act_quantize(r, torch.full((n,), rrange, device=gpu), limbs)
+    shift = torch.linspace(-1, 1, cout, device=gpu)
+    kw = dict(relu=True, want_f32=False, residual_q=rq, residual_range=rrange)
+    ref = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, relu=True)
+    cfgs = _halo_cfgs(ops, limbs, cin, cout)
+    assert cfgs
+    for frac in (3.0, 0.5):
+        rng = (float(ref.abs().max()) + rrange) * frac
+        ovf0 = torch.zeros(1, dtype=torch.int32, device=gpu)
+        _, yq0 = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, tile_cfg=-1, emit_range=rng,
+                              overflow=ovf0, **kw)
+        if frac < 1:
+            assert int(ovf0.item()) == 1
+        for c in cfgs:
+            ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+            _, yq = ops.conv2d_q(xq, am, codes, offset, 3, 3, 1, 1, step, shift, tile_cfg=c, emit_range=rng,
+                                 overflow=ovf, **kw)
+            assert torch.equal(yq, yq0), (c, frac)
+            assert torch.equal(ovf, ovf0), (c, frac)
+
+
 def test_halo_without_offsets_and_repeatable(gpu):
     """No weight offsets (the plain-code path) and 20 back-to-back launches of every halo config
     give the same bits (no race between the DMA of one chunk and the reads of the last)."""
@@ -115,7 +155,7 @@ def test_model_forward_halo_tiles_bitwise(gpu, arch, assign):
             gemm = [c for c in cands if ops.tile_kind(c) != ops.TILE_HALO3X3]
             # a halo tile only where the call is one it runs (lean, ReLU): key = n|h|w|cin|cout|kh|kw|
             # stride|pad|limbs|wlimbs|res_f32|emit_q|want_f32|res_q
-            lean = key[5] == 3 and key[7] == 1 and key[12] and not key[13] and not key[14] and not key[11]
+            lean = key[5] == 3 and key[7] == 1 and key[12] and not key[13] and not key[11]
             if kind == "halo" and halo and lean:
                 c = halo[0]
                 picked.append(c)

@@ -16,6 +16,11 @@ SHAPES = [  # name, cin, cout, k, stride, hin, residual, wlimbs
     ("c1_1024_256_14", 1024, 256, 1, 1, 14, False, 1),
     ("c3_256_1024_14r", 256, 1024, 1, 1, 14, True, 1),
     ("c2_512_512_7", 512, 512, 3, 1, 7, False, 1),
+    # BasicBlock conv2 (R18 / R34): 3x3 + the identity as limb planes, then ReLU
+    ("c2r_64_64_56", 64, 64, 3, 1, 56, True, 1),
+    ("c2r_128_128_28", 128, 128, 3, 1, 28, True, 1),
+    ("c2r_256_256_14", 256, 256, 3, 1, 14, True, 1),
+    ("c2r_512_512_7", 512, 512, 3, 1, 7, True, 1),
     ("c1_2048_512_7", 2048, 512, 1, 1, 7, False, 1),
     ("ds_1024_2048_14s2", 1024, 2048, 1, 2, 14, False, 3),
     ("ds_512_1024_28s2", 512, 1024, 1, 2, 28, False, 3),
